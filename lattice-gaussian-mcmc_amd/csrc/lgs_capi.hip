@@ -1,0 +1,713 @@
+// lgs_capi.hip -- the C-ABI of include/lgs.h: context, device-resident basis,
+// batching, host<->device staging and error reporting around the kernels of
+// lgs_kernels.hip.  No CPU compute path exists: every sample is drawn on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lgs.h"
+#include "lgs_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail(LGS_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                             \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    int reserve(size_t need) {
+        if (need <= bytes) return LGS_OK;
+        if (p) {
+            (void)hipFree(p);
+            p = nullptr;
+            bytes = 0;
+        }
+        if (need == 0) return LGS_OK;
+        hipError_t e = hipMalloc(&p, need);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(LGS_ERR_NOMEM, "hipMalloc(%zu) failed: %s", need, hipGetErrorString(e));
+        }
+        bytes = need;
+        return LGS_OK;
+    }
+    template <typename T>
+    T* as() const {
+        return (T*)p;
+    }
+};
+
+struct Timer {
+    int kernel;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct lgs_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    // basis
+    int64_t d = 0;
+    double sigma = 0;
+    int precision = 10;
+    uint32_t basis_flags = 0;
+    int panel = 32;
+    bool has_B = false;
+    DevBuf R, RP, RC, BT, coord;  // coord: cp | rii | sig | sig_ref | lterm (5 x d)
+    // scratch
+    DevBuf Z, LW, V, sel, fsel, cnt, ccnt, flags, stage_a, stage_b, stage_c, stage_d, stage_e,
+        stage_f, stage_g, vs;
+    int64_t max_props = 1 << 18;
+    // timing
+    bool timing = false;
+    double t_ms[4] = {0, 0, 0, 0};
+    int64_t t_n[4] = {0, 0, 0, 0};
+    std::vector<Timer> pending;
+    std::vector<hipEvent_t> pool;
+};
+
+namespace {
+
+int check_ctx(lgs_ctx* c, bool need_basis = true) {
+    if (!c) return fail(LGS_ERR_INVALID, "null context");
+    if (need_basis && c->d <= 0) return fail(LGS_ERR_STATE, "no basis loaded (lgs_set_basis)");
+    HIP_TRY(hipSetDevice(c->device));
+    return LGS_OK;
+}
+
+hipEvent_t get_event(lgs_ctx* c) {
+    if (!c->pool.empty()) {
+        hipEvent_t e = c->pool.back();
+        c->pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+struct Scope {  // times one launch when timing is enabled
+    lgs_ctx* c;
+    int k;
+    hipEvent_t a = nullptr;
+    Scope(lgs_ctx* c_, int k_) : c(c_), k(k_) {
+        if (c->timing) {
+            a = get_event(c);
+            (void)hipEventRecord(a, c->stream);
+        }
+    }
+    ~Scope() {
+        if (c->timing && a) {
+            hipEvent_t b = get_event(c);
+            (void)hipEventRecord(b, c->stream);
+            c->pending.push_back({k, a, b});
+        }
+    }
+};
+
+int finish(lgs_ctx* c) {  // sync, fold timers, report kernel flags
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (auto& t : c->pending) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+            c->t_ms[t.kernel] += ms;
+            c->t_n[t.kernel] += 1;
+        }
+        c->pool.push_back(t.a);
+        c->pool.push_back(t.b);
+    }
+    c->pending.clear();
+    unsigned int f = 0;
+    HIP_TRY(hipMemcpy(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost));
+    if (f & lgs::kFlagNonFinite)
+        return fail(LGS_ERR_NONFINITE, "non-finite conditional mean (reference raises ValueError)");
+    if (f & lgs::kFlagOverflow)
+        return fail(LGS_ERR_OVERFLOW, "coefficient |z| >= 2^31: rerun with LGS_Z64");
+    return LGS_OK;
+}
+
+int reset_flags(lgs_ctx* c) {
+    int rc = c->flags.reserve(16);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(c->flags.p, 0, 16, c->stream));
+    return LGS_OK;
+}
+
+lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
+    lgs::KleinArgs a{};
+    const double* co = c->coord.as<double>();
+    const int64_t d = c->d;
+    a.d = (int)d;
+    a.precision = c->precision;
+    a.linear_probs = (c->basis_flags & LGS_BASIS_LINEAR_PROBS) ? 1 : 0;
+    a.cp = co;
+    a.rii = co + d;
+    a.sig = co + 2 * d;
+    a.sig_ref = co + 3 * d;
+    a.lterm = co + 4 * d;
+    a.sigma = c->sigma;
+    a.seed = seed;
+    a.flags = c->flags.as<unsigned int>();
+    return a;
+}
+
+int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, bool z64, void* Z) {
+    Scope s(c, 0);
+    HIP_TRY(lgs::launch::klein(a, c->R.as<double>(), c->RP.as<double>(), c->RC.as<double>(),
+                               c->panel, exact, wl, z64, Z, c->stream));
+    return LGS_OK;
+}
+
+int run_bz(lgs_ctx* c, const void* Z, bool z64, int64_t ldz, int64_t n, double* V) {
+    if (!c->has_B) return fail(LGS_ERR_STATE, "lattice points need B (lgs_set_basis B != NULL)");
+    Scope s(c, 1);
+    HIP_TRY(lgs::launch::bz(Z, z64, ldz, c->BT.as<double>(), (int)c->d, n, V, c->d, c->stream));
+    return LGS_OK;
+}
+
+hipMemcpyKind kind_of(bool dev_dst, bool dev_src) {
+    if (dev_dst && dev_src) return hipMemcpyDeviceToDevice;
+    if (dev_dst) return hipMemcpyHostToDevice;
+    if (dev_src) return hipMemcpyDeviceToHost;
+    return hipMemcpyHostToHost;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lgs_version(void) { return 100; }
+
+const char* lgs_last_error(void) { return g_err.c_str(); }
+
+int lgs_create(lgs_ctx** out, int device) {
+    if (!out) return fail(LGS_ERR_INVALID, "null out pointer");
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n)
+        return fail(LGS_ERR_INVALID, "device %d out of range (%d devices)", device, n);
+    HIP_TRY(hipSetDevice(device));
+    lgs_ctx* c = new lgs_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(LGS_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    c->stream = c->own;
+    if (const char* p = getenv("LGS_PANEL")) c->panel = atoi(p) == 16 ? 16 : 32;
+    if (const char* m = getenv("LGS_MAX_PROPOSALS")) {
+        long long v = atoll(m);
+        if (v >= 64) c->max_props = v;
+    }
+    *out = c;
+    return LGS_OK;
+}
+
+int lgs_destroy(lgs_ctx* c) {
+    if (!c) return LGS_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& t : c->pending) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    for (auto e : c->pool) (void)hipEventDestroy(e);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+    return LGS_OK;
+}
+
+int lgs_set_stream(lgs_ctx* c, void* s) {
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    c->stream = s ? (hipStream_t)s : c->own;
+    return LGS_OK;
+}
+
+int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, const double* B,
+                  double sigma, int32_t precision, uint32_t flags) {
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    if (d <= 0 || d > (1 << 20)) return fail(LGS_ERR_INVALID, "dimension %lld out of range", (long long)d);
+    if (!R || !cprime) return fail(LGS_ERR_INVALID, "R and cprime are required");
+    if (!(sigma > 0) || !std::isfinite(sigma))
+        return fail(LGS_ERR_INVALID, "Standard deviation must be positive, got %g", sigma);
+    if (precision <= 0) return fail(LGS_ERR_INVALID, "precision must be positive");
+    const int PB = c->panel;
+    const size_t dd = (size_t)d;
+    // per-coordinate parameters (klein.py:195-211, 255-263)
+    std::vector<double> co(5 * dd);
+    for (size_t i = 0; i < dd; ++i) {
+        const double rii = R[i * dd + i];
+        if (rii == 0.0 || !std::isfinite(rii))
+            return fail(LGS_ERR_INVALID, "R[%zu,%zu] must be finite and non-zero", i, i);
+        const double sref = sigma / std::fabs(rii);
+        double s = sref;
+        if (sref < 1e-10)
+            s = 0.0;  // deterministic rounding
+        else if (sref > 1e10)
+            s = std::min(sref, 1e6);
+        co[i] = cprime[i];
+        co[dd + i] = rii;
+        co[2 * dd + i] = s;
+        co[3 * dd + i] = sref;
+        co[4 * dd + i] = 0.5 * std::log(2.0 * M_PI) + std::log(sref);
+    }
+    // panel layouts (lgs_kernels.hip, klein_panel_kernel)
+    const int64_t npan = (d + PB - 1) / PB;
+    size_t rp_elems = (size_t)PB * PB * (size_t)(npan * (npan - 1) / 2);
+    std::vector<double> rp(std::max<size_t>(rp_elems, 1), 0.0);
+    for (int64_t pk = 0; pk < npan; ++pk) {
+        const int64_t p_hi = d - pk * PB;
+        const size_t off = (size_t)PB * PB * (size_t)(pk * (pk - 1) / 2);
+        for (int64_t j = p_hi; j < d; ++j)
+            for (int r = 0; r < PB; ++r) {
+                const int64_t row = p_hi - PB + r;
+                rp[off + (size_t)(j - p_hi) * PB + r] = row >= 0 ? R[(size_t)row * dd + j] : 0.0;
+            }
+    }
+    std::vector<double> rcv(dd * (PB - 1), 0.0);
+    for (int64_t i = 0; i < d; ++i) {
+        const int64_t pk = (d - 1 - i) / PB;
+        const int64_t p_lo = std::max<int64_t>(0, d - (pk + 1) * PB);
+        for (int m = 0; m < PB - 1; ++m) {
+            const int64_t row = i - 1 - m;
+            rcv[(size_t)i * (PB - 1) + m] = row >= p_lo ? R[(size_t)row * dd + i] : 0.0;
+        }
+    }
+    if ((rc = c->R.reserve(dd * dd * 8)) || (rc = c->RP.reserve(rp.size() * 8)) ||
+        (rc = c->RC.reserve(rcv.size() * 8)) || (rc = c->coord.reserve(co.size() * 8)))
+        return rc;
+    HIP_TRY(hipMemcpy(c->R.p, R, dd * dd * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->RP.p, rp.data(), rp.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->RC.p, rcv.data(), rcv.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->coord.p, co.data(), co.size() * 8, hipMemcpyHostToDevice));
+    c->has_B = B != nullptr;
+    if (B) {
+        std::vector<double> bt(dd * dd);
+        for (size_t r = 0; r < dd; ++r)
+            for (size_t k = 0; k < dd; ++k) bt[k * dd + r] = B[r * dd + k];
+        if ((rc = c->BT.reserve(dd * dd * 8))) return rc;
+        HIP_TRY(hipMemcpy(c->BT.p, bt.data(), dd * dd * 8, hipMemcpyHostToDevice));
+    }
+    c->d = d;
+    c->sigma = sigma;
+    c->precision = precision;
+    c->basis_flags = flags;
+    // proposals per launch: keep the coefficient store around <= 2 GiB
+    const int64_t cap = std::max<int64_t>(256, (int64_t)((size_t)2 << 30) / (8 * d));
+    if (!getenv("LGS_MAX_PROPOSALS")) c->max_props = std::min<int64_t>(std::max<int64_t>(cap, 256), 1 << 20);
+    return LGS_OK;
+}
+
+int lgs_klein(lgs_ctx* c, uint64_t seed, uint64_t first, int64_t n, void* z_out, double* v_out,
+              double* logw_out, uint32_t flags) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (n < 0) return fail(LGS_ERR_INVALID, "n < 0");
+    if (n == 0) return LGS_OK;
+    const bool dev = flags & LGS_DEVICE_PTRS, z64 = flags & LGS_Z64,
+               cm = flags & LGS_COORD_MAJOR, exact = flags & LGS_EXACT_ORDER,
+               wl = flags & LGS_WANG_LING;
+    if (v_out && !c->has_B) return fail(LGS_ERR_STATE, "v_out requires B");
+    const int64_t d = c->d;
+    const size_t zb = z64 ? 8 : 4;
+    if ((rc = reset_flags(c))) return rc;
+    const int64_t chunk = std::min<int64_t>(n, c->max_props);
+    // direct device coordinate-major output: the kernel writes straight into z_out
+    const bool direct = dev && cm && z_out;
+    if (!direct && (rc = c->Z.reserve((size_t)chunk * d * zb))) return rc;
+    if ((rc = c->LW.reserve((size_t)chunk * 8))) return rc;
+    if (!dev) {
+        if (z_out && (rc = c->stage_a.reserve((size_t)chunk * d * zb))) return rc;
+        if (v_out && (rc = c->V.reserve((size_t)chunk * d * 8))) return rc;
+    }
+    for (int64_t off = 0; off < n; off += chunk) {
+        const int64_t m = std::min<int64_t>(chunk, n - off);
+        lgs::KleinArgs a = base_args(c, seed);
+        a.counter_mode = 0;
+        a.base = first + (uint64_t)off;
+        a.n = m;
+        void* Zp;
+        if (direct) {
+            Zp = (char*)z_out + (size_t)off * zb;
+            a.ldz = n;
+        } else {
+            Zp = c->Z.p;
+            a.ldz = m;
+        }
+        a.LW = logw_out ? (dev ? logw_out + off : c->LW.as<double>()) : nullptr;
+        if ((rc = run_klein(c, a, exact, wl, z64, Zp))) return rc;
+        if (z_out && !direct) {
+            if (cm) {  // coordinate-major output with host pointers or via staging
+                for (int64_t i = 0; i < d; ++i)
+                    HIP_TRY(hipMemcpy2DAsync((char*)z_out + ((size_t)i * n + off) * zb, 0,
+                                             (char*)Zp + (size_t)i * m * zb, 0, m * zb, 1,
+                                             kind_of(dev, true), c->stream));
+            } else {
+                void* dst = dev ? (char*)z_out + (size_t)off * d * zb : c->stage_a.p;
+                HIP_TRY(lgs::launch::transpose_out(Zp, z64, a.ldz, m, (int)d, dst, z64, c->stream));
+                if (!dev)
+                    HIP_TRY(hipMemcpyAsync((char*)z_out + (size_t)off * d * zb, dst, (size_t)m * d * zb,
+                                           hipMemcpyDeviceToHost, c->stream));
+            }
+        }
+        if (v_out) {
+            double* V = dev ? v_out + (size_t)off * d : c->V.as<double>();
+            if ((rc = run_bz(c, Zp, z64, a.ldz, m, V))) return rc;
+            if (!dev)
+                HIP_TRY(hipMemcpyAsync(v_out + (size_t)off * d, V, (size_t)m * d * 8,
+                                       hipMemcpyDeviceToHost, c->stream));
+        }
+        if (logw_out && !dev)
+            HIP_TRY(hipMemcpyAsync(logw_out + off, a.LW, (size_t)m * 8, hipMemcpyDeviceToHost,
+                                   c->stream));
+        if (!dev) {  // host staging buffers are reused by the next chunk
+            if ((rc = finish(c))) return rc;
+        }
+    }
+    return finish(c);
+}
+
+int lgs_lattice_points(lgs_ctx* c, int64_t n, const void* z, double* v_out, uint32_t flags) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? LGS_OK : fail(LGS_ERR_INVALID, "n < 0");
+    if (!z || !v_out) return fail(LGS_ERR_INVALID, "null buffer");
+    const bool dev = flags & LGS_DEVICE_PTRS, z64 = flags & LGS_Z64, cm = flags & LGS_COORD_MAJOR;
+    const int64_t d = c->d;
+    const size_t zb = z64 ? 8 : 4;
+    if ((rc = reset_flags(c))) return rc;
+    const void* Zc = z;
+    if (!dev || !cm) {
+        if ((rc = c->Z.reserve((size_t)n * d * zb)) || (rc = c->stage_a.reserve((size_t)n * d * zb)))
+            return rc;
+        const void* src = z;
+        if (!dev) {
+            HIP_TRY(hipMemcpyAsync(c->stage_a.p, z, (size_t)n * d * zb, hipMemcpyHostToDevice, c->stream));
+            src = c->stage_a.p;
+        }
+        if (cm) {
+            Zc = src;
+        } else {
+            HIP_TRY(lgs::launch::to_coord_major(src, z64, n, (int)d, c->Z.p, z64, n, c->stream));
+            Zc = c->Z.p;
+        }
+    }
+    double* V = v_out;
+    if (!dev) {
+        if ((rc = c->V.reserve((size_t)n * d * 8))) return rc;
+        V = c->V.as<double>();
+    }
+    if ((rc = run_bz(c, Zc, z64, n, n, V))) return rc;
+    if (!dev) HIP_TRY(hipMemcpyAsync(v_out, V, (size_t)n * d * 8, hipMemcpyDeviceToHost, c->stream));
+    return finish(c);
+}
+
+int lgs_log_density(lgs_ctx* c, int64_t n, const void* z, double* out, uint32_t flags) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (n <= 0) return n == 0 ? LGS_OK : fail(LGS_ERR_INVALID, "n < 0");
+    if (!z || !out) return fail(LGS_ERR_INVALID, "null buffer");
+    const bool dev = flags & LGS_DEVICE_PTRS, z64 = flags & LGS_Z64, cm = flags & LGS_COORD_MAJOR;
+    const int64_t d = c->d;
+    const size_t zb = z64 ? 8 : 4;
+    if ((rc = reset_flags(c))) return rc;
+    const void* Zc = z;
+    if (!dev || !cm) {
+        if ((rc = c->Z.reserve((size_t)n * d * zb)) || (rc = c->stage_a.reserve((size_t)n * d * zb)))
+            return rc;
+        const void* src = z;
+        if (!dev) {
+            HIP_TRY(hipMemcpyAsync(c->stage_a.p, z, (size_t)n * d * zb, hipMemcpyHostToDevice, c->stream));
+            src = c->stage_a.p;
+        }
+        if (cm) {
+            Zc = src;
+        } else {
+            HIP_TRY(lgs::launch::to_coord_major(src, z64, n, (int)d, c->Z.p, z64, n, c->stream));
+            Zc = c->Z.p;
+        }
+    }
+    double* o = out;
+    if (!dev) {
+        if ((rc = c->LW.reserve((size_t)n * 8))) return rc;
+        o = c->LW.as<double>();
+    }
+    lgs::KleinArgs a = base_args(c, 0);
+    a.n = n;
+    a.ldz = n;
+    HIP_TRY(lgs::launch::log_density(a, c->R.as<double>(), Zc, z64, o, c->stream));
+    if (!dev) HIP_TRY(hipMemcpyAsync(out, o, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    return finish(c);
+}
+
+int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64_t first_step,
+             int64_t n_steps, int32_t thin, void* z_state, double* logw_state, int32_t* state_init,
+             int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
+             uint32_t flags) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (nc < 0 || n_steps < 0 || thin < 1) return fail(LGS_ERR_INVALID, "bad nc/n_steps/thin");
+    if (first_step < 1) return fail(LGS_ERR_INVALID, "first_step must be >= 1 (step 0 is the initial draw)");
+    if (!z_state || !logw_state || !state_init || !accepts)
+        return fail(LGS_ERR_INVALID, "z_state, logw_state, state_init and accepts are required");
+    const bool dev = flags & LGS_DEVICE_PTRS, z64 = flags & LGS_Z64,
+               cm = flags & LGS_COORD_MAJOR, exact = flags & LGS_EXACT_ORDER,
+               wl = flags & LGS_WANG_LING;
+    if (v_samples && !c->has_B) return fail(LGS_ERR_STATE, "v_samples requires B");
+    if (v_samples && !dev)
+        return fail(LGS_ERR_INVALID, "v_samples needs LGS_DEVICE_PTRS (use lgs_lattice_points on z_samples)");
+    if (z_samples && cm)
+        return fail(LGS_ERR_INVALID, "z_samples is row-major (n_chains x n_keep x d) only");
+    if (nc == 0) return LGS_OK;
+    if (first_chain + (uint64_t)nc > (1ull << 32) || first_step + (uint64_t)n_steps > (1ull << 32))
+        return fail(LGS_ERR_INVALID, "chain / step counters must stay below 2^32");
+    const int64_t d = c->d;
+    const size_t zb = z64 ? 8 : 4;
+    const int64_t n_keep = n_steps / thin;
+    if ((rc = reset_flags(c))) return rc;
+
+    // ---- block of T steps (a multiple of thin) per Klein launch
+    int64_t T = std::max<int64_t>(1, c->max_props / nc);
+    if (T < n_steps) T = std::max<int64_t>(thin, (T / thin) * thin);
+    T = std::min<int64_t>(T, std::max<int64_t>(n_steps, 1));
+    const int64_t np = nc * T;
+    const int64_t kmax = std::max<int64_t>(T / thin, 1);
+    if ((rc = c->Z.reserve((size_t)np * d * zb)) || (rc = c->LW.reserve((size_t)np * 8)) ||
+        (rc = c->sel.reserve((size_t)std::max<int64_t>(nc * kmax, nc) * 8)) ||
+        (rc = c->fsel.reserve((size_t)nc * 8)) || (rc = c->cnt.reserve((size_t)np * 4)) ||
+        (rc = c->ccnt.reserve((size_t)nc * 4)))
+        return rc;
+    if (v_samples && ((rc = c->V.reserve((size_t)np * d * 8)) || (rc = c->vs.reserve((size_t)nc * d * 8))))
+        return rc;
+
+    // ---- device views of the chain state (staged through device buffers for host pointers)
+    void* zs = z_state;
+    double* lws = logw_state;
+    int32_t* init = state_init;
+    int64_t* acc = accepts;
+    std::vector<int32_t> h_init(nc);
+    if (dev) {
+        HIP_TRY(hipMemcpyAsync(h_init.data(), state_init, nc * 4, hipMemcpyDeviceToHost, c->stream));
+    } else {
+        memcpy(h_init.data(), state_init, nc * 4);
+        if ((rc = c->stage_a.reserve((size_t)nc * d * zb)) || (rc = c->stage_b.reserve((size_t)nc * 8)) ||
+            (rc = c->stage_c.reserve((size_t)nc * 4)) || (rc = c->stage_d.reserve((size_t)nc * 8)))
+            return rc;
+        zs = c->stage_a.p;
+        lws = c->stage_b.as<double>();
+        init = c->stage_c.as<int32_t>();
+        acc = c->stage_d.as<int64_t>();
+        HIP_TRY(hipMemcpyAsync(zs, z_state, (size_t)nc * d * zb, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(lws, logw_state, nc * 8, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(init, state_init, nc * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(acc, accepts, nc * 8, hipMemcpyHostToDevice, c->stream));
+    }
+    unsigned long long* mom = nullptr;
+    if (moments) {
+        if (dev) {
+            mom = (unsigned long long*)moments;
+        } else {
+            if ((rc = c->stage_e.reserve((size_t)2 * d * 8))) return rc;
+            mom = c->stage_e.as<unsigned long long>();
+            HIP_TRY(hipMemcpyAsync(mom, moments, (size_t)2 * d * 8, hipMemcpyHostToDevice, c->stream));
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+
+    // ---- initial draws (counter step 0) for uninitialised chains (imhk.py:126-139)
+    bool any_uninit = false;
+    for (int64_t i = 0; i < nc; ++i) any_uninit |= (h_init[i] == 0);
+    if (any_uninit) {
+        lgs::KleinArgs a = base_args(c, seed);
+        a.counter_mode = 1;
+        a.chain0 = (uint32_t)first_chain;
+        a.step0 = 0;
+        a.nc = nc;
+        a.n = nc;
+        a.ldz = nc;
+        a.LW = c->LW.as<double>();
+        if ((rc = run_klein(c, a, exact, wl, z64, c->Z.p))) return rc;
+        std::vector<int64_t> s(nc);
+        for (int64_t i = 0; i < nc; ++i) s[i] = h_init[i] ? -1 : i;
+        HIP_TRY(hipMemcpyAsync(c->sel.p, s.data(), nc * 8, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(lgs::launch::gather_z(c->Z.p, z64, nc, c->sel.as<int64_t>(), nc, 1, zs, cm, nc,
+                                      (int)d, zs, cm, c->stream));
+        std::vector<double> h_lw(nc), cur(nc);
+        HIP_TRY(hipMemcpyAsync(h_lw.data(), c->LW.p, nc * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(cur.data(), lws, nc * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (int64_t i = 0; i < nc; ++i)
+            if (!h_init[i]) {
+                cur[i] = h_lw[i];
+                h_init[i] = 1;
+            }
+        HIP_TRY(hipMemcpyAsync(lws, cur.data(), nc * 8, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(init, h_init.data(), nc * 4, hipMemcpyHostToDevice, c->stream));
+    }
+
+    // ---- blocks
+    for (int64_t t0 = 0; t0 < n_steps; t0 += T) {
+        const int64_t Tb = std::min<int64_t>(T, n_steps - t0);
+        const int64_t npb = nc * Tb;
+        const int64_t first_keep = t0 / thin;  // t0 is a multiple of thin
+        const int64_t kb = std::min<int64_t>(Tb / thin, n_keep - first_keep);
+        lgs::KleinArgs a = base_args(c, seed);
+        a.counter_mode = 1;
+        a.chain0 = (uint32_t)first_chain;
+        a.step0 = (uint32_t)(first_step + (uint64_t)t0);
+        a.nc = nc;
+        a.n = npb;
+        a.ldz = npb;
+        a.LW = c->LW.as<double>();
+        if ((rc = run_klein(c, a, exact, wl, z64, c->Z.p))) return rc;
+        if (v_samples && kb > 0) {  // lattice points of the carried states, before they move
+            const void* zcm = zs;
+            if (!cm) {
+                if ((rc = c->stage_f.reserve((size_t)nc * d * zb))) return rc;
+                HIP_TRY(lgs::launch::to_coord_major(zs, z64, nc, (int)d, c->stage_f.p, z64, nc, c->stream));
+                zcm = c->stage_f.p;
+            }
+            if ((rc = run_bz(c, zcm, z64, nc, nc, c->vs.as<double>()))) return rc;
+        }
+        if (moments) HIP_TRY(hipMemsetAsync(c->cnt.p, 0, (size_t)npb * 4, c->stream));
+        lgs::AcceptArgs aa{};
+        aa.nc = nc;
+        aa.T = Tb;
+        aa.thin = thin;
+        aa.n_keep = std::max<int64_t>(kb, 1);
+        aa.seed = seed;
+        aa.chain0 = (uint32_t)first_chain;
+        aa.step0 = a.step0;
+        aa.LW = c->LW.as<double>();
+        aa.lw_state = lws;
+        aa.accepts = acc;
+        aa.sel = (z_samples || v_samples) && kb > 0 ? c->sel.as<int64_t>() : nullptr;
+        aa.final_sel = c->fsel.as<int64_t>();
+        aa.cnt = moments ? c->cnt.as<int32_t>() : nullptr;
+        aa.cnt_carry = moments ? c->ccnt.as<int32_t>() : nullptr;
+        {
+            Scope s(c, 2);
+            HIP_TRY(lgs::launch::accept(aa, c->stream));
+        }
+        if (moments) {
+            Scope s(c, 3);
+            HIP_TRY(lgs::launch::moments(c->Z.p, z64, npb, c->cnt.as<int32_t>(), npb, (int)d, mom, c->stream));
+            HIP_TRY(lgs::launch::moments_carry(zs, z64, cm, nc, (int)d, c->ccnt.as<int32_t>(), mom, c->stream));
+        }
+        if (z_samples && kb > 0) {
+            // kept states -> rows (chain, first_keep + k) of the n_chains x n_keep x d output
+            const int64_t nq = nc * kb;
+            void* out;
+            if (dev && !cm && kb == n_keep) {
+                out = z_samples;
+            } else {
+                if ((rc = c->stage_f.reserve((size_t)nq * d * zb))) return rc;
+                out = c->stage_f.p;
+            }
+            HIP_TRY(lgs::launch::gather_z(c->Z.p, z64, npb, c->sel.as<int64_t>(), nq, kb, zs, cm, nc,
+                                          (int)d, out, 0, c->stream));
+            if (out != z_samples) {
+                HIP_TRY(hipMemcpy2DAsync((char*)z_samples + (size_t)first_keep * d * zb,
+                                         (size_t)n_keep * d * zb, out, (size_t)kb * d * zb,
+                                         (size_t)kb * d * zb, nc, kind_of(dev, true), c->stream));
+            }
+        }
+        if (v_samples && kb > 0) {
+            const int64_t nq = nc * kb;
+            if ((rc = run_bz(c, c->Z.p, z64, npb, npb, c->V.as<double>()))) return rc;
+            double* out;
+            if (kb == n_keep) {
+                out = v_samples;
+            } else {
+                if ((rc = c->stage_g.reserve((size_t)nq * d * 8))) return rc;
+                out = c->stage_g.as<double>();
+            }
+            HIP_TRY(lgs::launch::gather_v(c->V.as<double>(), c->sel.as<int64_t>(), nq, kb,
+                                          c->vs.as<double>(), (int)d, out, c->stream));
+            if (out != v_samples)
+                HIP_TRY(hipMemcpy2DAsync(v_samples + (size_t)first_keep * d, (size_t)n_keep * d * 8, out,
+                                         (size_t)kb * d * 8, (size_t)kb * d * 8, nc,
+                                         hipMemcpyDeviceToDevice, c->stream));
+        }
+        // chain states after the block (in place; carried chains keep their row)
+        HIP_TRY(lgs::launch::gather_z(c->Z.p, z64, npb, c->fsel.as<int64_t>(), nc, 1, zs, cm, nc,
+                                      (int)d, zs, cm, c->stream));
+        if ((rc = finish(c))) return rc;
+    }
+    if (!dev) {
+        HIP_TRY(hipMemcpyAsync(z_state, zs, (size_t)nc * d * zb, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(logw_state, lws, nc * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(state_init, init, nc * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(accepts, acc, nc * 8, hipMemcpyDeviceToHost, c->stream));
+        if (moments)
+            HIP_TRY(hipMemcpyAsync(moments, mom, (size_t)2 * d * 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    return finish(c);
+}
+
+int lgs_timing_enable(lgs_ctx* c, int enable) {
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    c->timing = enable != 0;
+    for (int k = 0; k < 4; ++k) {
+        c->t_ms[k] = 0;
+        c->t_n[k] = 0;
+    }
+    return LGS_OK;
+}
+
+int lgs_timing_get(lgs_ctx* c, int kernel, double* ms, int64_t* n) {
+    if (!c) return fail(LGS_ERR_INVALID, "null context");
+    if (kernel < 0 || kernel > 3) return fail(LGS_ERR_INVALID, "kernel id 0..3");
+    if (ms) *ms = c->t_ms[kernel];
+    if (n) *n = c->t_n[kernel];
+    return LGS_OK;
+}
+
+int lgs_device_info(lgs_ctx* c, char* name, int name_len, int* n_cu, int64_t* hbm) {
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    hipDeviceProp_t p;
+    HIP_TRY(hipGetDeviceProperties(&p, c->device));
+    if (name && name_len > 0) {
+        snprintf(name, (size_t)name_len, "%s (%s)", p.name, p.gcnArchName);
+    }
+    if (n_cu) *n_cu = p.multiProcessorCount;
+    if (hbm) *hbm = (int64_t)p.totalGlobalMem;
+    return LGS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,143 @@
+// lgs_device.h -- device-side building blocks of the Klein / IMHK path (gfx950).
+//
+//  * Philox4x32-10 counter RNG + NumPy's 53-bit double conversion: replaces the
+//    single MT19937 draw of np.random.choice (reference src/samplers/klein.py:175)
+//    and np.random.rand (src/samplers/imhk.py:167).  Counter layout: DESIGN.md §RNG.
+//  * SampleZ: the 1-D discrete Gaussian of klein.py:101-179 (support window,
+//    table, cumulative search) evaluated per lane.
+//
+// The translation unit is compiled with -ffp-contract=off: every a*b+c below is
+// two roundings, exactly like NumPy, unless written as an explicit fma().
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lgs {
+
+constexpr uint32_t kTagCoord = 0;
+constexpr uint32_t kTagAccept = 1;
+
+struct U4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint32_t lo0 = 0xD2511F53u * c0;
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0;
+        const uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+    }
+    return {c0, c1, c2, c3};
+}
+
+// NumPy legacy double: ((a >> 5) * 2^26 + (b >> 6)) / 2^53 (exact in fp64).
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// Uniform of the IMHK acceptance test (ctr = {0, step, chain, 1}).
+__device__ __forceinline__ double accept_uniform(uint64_t seed, uint32_t step, uint32_t chain) {
+    U4 w = philox4x32_10(0u, step, chain, kTagAccept, (uint32_t)seed, (uint32_t)(seed >> 32));
+    return u53(w.x, w.y);
+}
+
+// Per-lane coordinate uniform stream: slot k = d-1-i, two slots per Philox call.
+struct CoordStream {
+    uint32_t k0, k1, step, chain;
+    uint32_t pair;  // cached pair index (0xffffffff = none)
+    U4 w;
+    __device__ __forceinline__ void init(uint64_t seed, uint32_t step_, uint32_t chain_) {
+        k0 = (uint32_t)seed;
+        k1 = (uint32_t)(seed >> 32);
+        step = step_;
+        chain = chain_;
+        pair = 0xffffffffu;
+    }
+    __device__ __forceinline__ double u(uint32_t slot) {
+        const uint32_t p = slot >> 1;
+        if (p != pair) {
+            w = philox4x32_10(p, step, chain, kTagCoord, k0, k1);
+            pair = p;
+        }
+        return (slot & 1u) ? u53(w.z, w.w) : u53(w.x, w.y);
+    }
+};
+
+// ------------------------------------------------------------------ SampleZ
+// Support window of _compute_1d_probabilities (klein.py:113-128).
+__device__ __forceinline__ void support_window(double mu, double sig, int precision, int64_t& lo,
+                                               int64_t& hi) {
+    const double rf = (sig < 0.1) ? (double)(precision > 3 ? precision : 3) : (double)precision;
+    lo = (int64_t)floor(mu - rf * sig);
+    hi = (int64_t)ceil(mu + rf * sig);
+    if (hi - lo > 1000) {
+        const int64_t c = (int64_t)rint(mu);  // np.round: half to even
+        lo = c - 500;
+        hi = c + 500;
+    }
+}
+
+struct SampleZOut {
+    int64_t z;
+    double log_norm;  // log sum_k exp(-(k-mu)^2/(2 sig^2)) over the window (Wang-Ling weight)
+};
+
+// Decision of klein.py:143-179 for uniform u: the smallest k in the window with
+// cumsum(p)[k] > u * sum(p), p_k proportional to exp(-((k-mu)/sig)^2 / 2).
+// The table is max-shifted (w = 1 at the k nearest mu) instead of normalised by
+// scipy's logsumexp: the normalisation cancels in cdf = cumsum / cumsum[-1], so
+// the decision is the reference's up to ulp-level rounding of the boundaries.
+// Two passes over the window (sum, then cumulative walk); no table storage.
+__device__ __forceinline__ SampleZOut sample_z_table(double mu, double sig, int precision,
+                                                     bool linear_probs, double u) {
+    int64_t lo, hi;
+    support_window(mu, sig, precision, lo, hi);
+    int64_t ks = (int64_t)rint(mu);
+    ks = ks < lo ? lo : (ks > hi ? hi : ks);
+    const double ts = ((double)ks - mu) / sig;
+    const double shift = -0.5 * (ts * ts);
+    SampleZOut out;
+    if (linear_probs && exp(shift) == 0.0) {
+        // use_log_space=False: every probability underflows -> NaN -> the
+        // reference's ValueError fallback round(mean) (klein.py:176-179).
+        out.z = (int64_t)rint(mu);
+        out.log_norm = -INFINITY;
+        return out;
+    }
+    const double flo = (double)lo;
+    const int n = (int)(hi - lo) + 1;
+    double S = 0.0;
+    for (int k = 0; k < n; ++k) {
+        const double t = ((flo + (double)k) - mu) / sig;
+        S += exp(-0.5 * (t * t) - shift);
+    }
+    const double target = u * S;
+    double C = 0.0;
+    int64_t z = hi;
+    for (int k = 0; k < n; ++k) {
+        const double t = ((flo + (double)k) - mu) / sig;
+        C += exp(-0.5 * (t * t) - shift);
+        if (C > target) {
+            z = lo + k;
+            break;
+        }
+    }
+    out.z = z;
+    out.log_norm = shift + log(S);
+    return out;
+}
+
+}  // namespace lgs

@@ -1,0 +1,80 @@
+// lgs_kernels.h -- internal interface between the C-ABI (lgs_capi.hip) and the
+// kernels (lgs_kernels.hip).  Not part of the public ABI (see include/lgs.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lgs {
+
+constexpr unsigned int kFlagNonFinite = 1u;  // a conditional mean was NaN/inf
+constexpr unsigned int kFlagOverflow = 2u;   // |z| >= 2^31 with an int32 store
+
+// Per-launch arguments of the Klein samplers.  Per-coordinate arrays (length d):
+//   cp      c' = Q^T c
+//   rii     R_ii (> 0 after the sign fix of klein.py:69-73)
+//   sig     effective SampleZ sigma: sigma/R_ii, clamped to 1e6 above 1e10,
+//           0 when sigma/R_ii < 1e-10 (deterministic rounding)
+//   sig_ref sigma/R_ii unclamped (reference-mode weight, klein.py:255-263)
+//   lterm   0.5*log(2*pi) + log(sig_ref)
+struct KleinArgs {
+    int d;
+    int precision;
+    int linear_probs;
+    int counter_mode;  // 0: lane p -> sample base+p; 1: chain0 + p%nc, step0 + p/nc
+    const double* cp;
+    const double* rii;
+    const double* sig;
+    const double* sig_ref;
+    const double* lterm;
+    double sigma;
+    uint64_t seed;
+    uint64_t base;
+    uint32_t chain0;
+    uint32_t step0;
+    int64_t nc;
+    int64_t n;
+    int64_t ldz;
+    double* LW;
+    unsigned int* flags;
+};
+
+struct AcceptArgs {
+    int64_t nc;
+    int64_t T;
+    int64_t thin;
+    int64_t n_keep;
+    uint64_t seed;
+    uint32_t chain0;
+    uint32_t step0;
+    const double* LW;
+    double* lw_state;
+    int64_t* accepts;
+    int64_t* sel;        // nullable, nc x n_keep
+    int64_t* final_sel;  // nc
+    int32_t* cnt;        // nullable, per proposal (zeroed by caller)
+    int32_t* cnt_carry;  // nullable, per chain
+};
+
+namespace launch {
+hipError_t klein(const KleinArgs& a, const double* R, const double* RP, const double* RC,
+                 int panel, bool exact, bool wl, bool z64, void* Z, hipStream_t st);
+hipError_t accept(const AcceptArgs& a, hipStream_t st);
+hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, bool z64, double* out,
+                       hipStream_t st);
+hipError_t moments(const void* Z, bool z64, int64_t ldz, const int32_t* cnt, int64_t n, int d,
+                   unsigned long long* mom, hipStream_t st);
+hipError_t moments_carry(const void* zs, bool z64, int coord_major, int64_t nc, int d,
+                         const int32_t* cc, unsigned long long* mom, hipStream_t st);
+hipError_t gather_z(const void* Z, bool z64, int64_t ldz, const int64_t* sel, int64_t nq,
+                    int64_t q_per_chain, const void* zs, int zs_coord_major, int64_t nc, int d,
+                    void* out, int out_coord_major, hipStream_t st);
+hipError_t gather_v(const double* V, const int64_t* sel, int64_t nq, int64_t q_per_chain,
+                    const double* vs, int d, double* out, hipStream_t st);
+hipError_t transpose_out(const void* Z, bool z64, int64_t ldz, int64_t n, int d, void* out,
+                         bool out64, hipStream_t st);
+hipError_t to_coord_major(const void* in, bool in64, int64_t n, int d, void* Z, bool z64,
+                          int64_t ldz, hipStream_t st);
+hipError_t bz(const void* Z, bool z64, int64_t ldz, const double* BT, int d, int64_t n, double* V,
+              int64_t ldv, hipStream_t st);
+}  // namespace launch
+}  // namespace lgs

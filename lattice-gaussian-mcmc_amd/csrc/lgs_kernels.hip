@@ -1,0 +1,591 @@
+// lgs_kernels.hip -- HIP/CDNA4 kernels of the Klein / IMHK hot path (gfx950).
+//
+//   klein_exact_kernel  Klein randomized nearest plane, reference arithmetic order
+//                       (klein.py:181-220: sequential j-ascending unfused fp64 sums),
+//                       one chain (sample) per lane.
+//   klein_panel_kernel  Same sampler, blocked: PB rows per panel, far-field
+//                       contributions left-looking from the coefficient store
+//                       (one coalesced load feeds PB FMAs), near field right-looking
+//                       in registers.  Default (fast) mode.
+//   imhk_accept_kernel  Metropolis test of imhk.py:141-177 over a block of steps,
+//                       one chain per lane (proposals are independent of the state).
+//   bz_gemm_kernel      v = B z for a batch (klein.py:218), fp64 MFMA 16x16x4.
+//   moments / gathers / transpose helpers.
+//
+// Coefficient store layout: Z[coord][lane] ("coordinate-major", ld = ldz) so that
+// every access of the sampler is a 64-lane coalesced row segment.
+//
+// Compiled with -ffp-contract=off (see lgs_device.h).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lgs_device.h"
+#include "lgs_kernels.h"
+
+namespace lgs {
+
+__device__ __forceinline__ void lane_counter(const KleinArgs& a, int64_t p, uint32_t& chain,
+                                             uint32_t& step) {
+    if (a.counter_mode == 0) {
+        const uint64_t s = a.base + (uint64_t)p;
+        chain = (uint32_t)s;
+        step = (uint32_t)(s >> 32);
+    } else {
+        chain = a.chain0 + (uint32_t)(p % a.nc);
+        step = a.step0 + (uint32_t)(p / a.nc);
+    }
+}
+
+// One coordinate's decision + weight bookkeeping, shared by both samplers.
+template <bool WL>
+__device__ __forceinline__ int64_t decide_coord(const KleinArgs& a, int i, double mu,
+                                                CoordStream& rs, double& lw,
+                                                unsigned int& flags) {
+    const double s = a.sig[i];
+    int64_t zi;
+    if (!isfinite(mu)) {
+        flags |= kFlagNonFinite;
+        return 0;
+    }
+    if (s == 0.0) {  // sigma_i < 1e-10: round, no draw (klein.py:201-204)
+        zi = (int64_t)rint(mu);
+    } else {
+        SampleZOut o = sample_z_table(mu, s, a.precision, a.linear_probs != 0,
+                                      rs.u((uint32_t)(a.d - 1 - i)));
+        zi = o.z;
+        if (WL) lw += o.log_norm;
+    }
+    if (!WL) {
+        // Reference-mode importance weight (imhk.py:102-124): log_gaussian_weight(Bz)
+        // - compute_log_density(Bz), with ||Bz - c||^2 = sum_i (R_ii (z_i - mu_i))^2.
+        const double res = (double)zi - mu;
+        const double ta = res * a.rii[i] / a.sigma;
+        const double tq = res / a.sig_ref[i];
+        lw += (-0.5 * (ta * ta)) - (-0.5 * (tq * tq) - a.lterm[i]);
+    }
+    return zi;
+}
+
+template <typename ZT>
+__device__ __forceinline__ void store_z(ZT* Z, size_t off, int64_t zi, unsigned int& flags) {
+    if (sizeof(ZT) == 4 && (zi > 2147483647LL || zi < -2147483648LL)) flags |= kFlagOverflow;
+    Z[off] = (ZT)zi;
+}
+
+// ------------------------------------------------------------ exact order
+template <typename ZT, bool WL>
+__global__ __launch_bounds__(256) void klein_exact_kernel(const KleinArgs a,
+                                                          const double* __restrict__ R,
+                                                          ZT* __restrict__ Z) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n) return;
+    uint32_t chain, step;
+    lane_counter(a, p, chain, step);
+    CoordStream rs;
+    rs.init(a.seed, step, chain);
+    const int d = a.d;
+    const size_t ldz = (size_t)a.ldz;
+    double lw = 0.0;
+    unsigned int flags = 0;
+    for (int i = d - 1; i >= 0; --i) {
+        const double* __restrict__ Ri = R + (size_t)i * d;
+        double cs = 0.0;
+        for (int j = i + 1; j < d; ++j) cs = cs + Ri[j] * (double)Z[(size_t)j * ldz + p];
+        const double mu = (a.cp[i] - cs) / a.rii[i];
+        const int64_t zi = decide_coord<WL>(a, i, mu, rs, lw, flags);
+        store_z(Z, (size_t)i * ldz + p, zi, flags);
+    }
+    if (a.LW) a.LW[p] = lw;
+    if (flags) atomicOr(a.flags, flags);
+}
+
+// ------------------------------------------------------------ panel (fast)
+// RP: far-field blocks, panel k (rows [p_hi-PB, p_hi), p_hi = d - k*PB) stores
+//     for j in [p_hi, d): PB doubles RP[off_k + (j-p_hi)*PB + r] = R[p_hi-PB+r][j]
+//     (0 for rows < 0); off_k = PB*PB*k*(k-1)/2.
+// RC: near-field columns, RC[i*(PB-1) + m] = R[i-1-m][i] if row i-1-m is in
+//     row i's panel, else 0.
+template <typename ZT, int PB, bool WL>
+__global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
+                                                          const double* __restrict__ RP,
+                                                          const double* __restrict__ RC,
+                                                          ZT* __restrict__ Z) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n) return;
+    uint32_t chain, step;
+    lane_counter(a, p, chain, step);
+    CoordStream rs;
+    rs.init(a.seed, step, chain);
+    const int d = a.d;
+    const size_t ldz = (size_t)a.ldz;
+    double lw = 0.0;
+    unsigned int flags = 0;
+    const int npan = (d + PB - 1) / PB;
+    double acc[PB];
+    for (int pk = 0; pk < npan; ++pk) {
+        const int p_hi = d - pk * PB;
+        const int rows = p_hi < PB ? p_hi : PB;
+#pragma unroll
+        for (int r = 0; r < PB; ++r) acc[r] = 0.0;
+        const double* __restrict__ rp = RP + (size_t)PB * PB * ((size_t)pk * (pk - 1) / 2);
+        int j = p_hi;
+        for (; j + 1 < d; j += 2) {
+            const double x0 = (double)Z[(size_t)j * ldz + p];
+            const double x1 = (double)Z[(size_t)(j + 1) * ldz + p];
+            const double* __restrict__ rj = rp + (size_t)(j - p_hi) * PB;
+#pragma unroll
+            for (int r = 0; r < PB; ++r) acc[r] = fma(rj[r], x0, acc[r]);
+#pragma unroll
+            for (int r = 0; r < PB; ++r) acc[r] = fma(rj[PB + r], x1, acc[r]);
+        }
+        if (j < d) {
+            const double x0 = (double)Z[(size_t)j * ldz + p];
+            const double* __restrict__ rj = rp + (size_t)(j - p_hi) * PB;
+#pragma unroll
+            for (int r = 0; r < PB; ++r) acc[r] = fma(rj[r], x0, acc[r]);
+        }
+        for (int s = 0; s < rows; ++s) {
+            const int i = p_hi - 1 - s;
+            const double mu = (a.cp[i] - acc[PB - 1]) / a.rii[i];
+            const int64_t zi = decide_coord<WL>(a, i, mu, rs, lw, flags);
+            store_z(Z, (size_t)i * ldz + p, zi, flags);
+            const double x = (double)zi;
+            const double* __restrict__ rc = RC + (size_t)i * (PB - 1);
+#pragma unroll
+            for (int k = 0; k < PB - 1; ++k) acc[k] = fma(rc[PB - 2 - k], x, acc[k]);
+#pragma unroll
+            for (int k = PB - 1; k >= 1; --k) acc[k] = acc[k - 1];
+            acc[0] = 0.0;
+        }
+    }
+    if (a.LW) a.LW[p] = lw;
+    if (flags) atomicOr(a.flags, flags);
+}
+
+// ------------------------------------------------------------ log density
+// compute_log_density (klein.py:222-271) of given coefficient vectors, reference
+// arithmetic order: sum_i -0.5*((z_i-mu_i)/sigma_i)^2 - (0.5*log(2pi) + log sigma_i)
+// - log_Z_i, where log_Z_i = logsumexp of the already-normalised table is 0 up to
+// rounding (taken as 0).
+template <typename ZT>
+__global__ __launch_bounds__(256) void log_density_kernel(const KleinArgs a,
+                                                          const double* __restrict__ R,
+                                                          const ZT* __restrict__ Z,
+                                                          double* __restrict__ out) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n) return;
+    const int d = a.d;
+    const size_t ldz = (size_t)a.ldz;
+    double lp = 0.0;
+    for (int i = d - 1; i >= 0; --i) {
+        const double* __restrict__ Ri = R + (size_t)i * d;
+        double cs = 0.0;
+        for (int j = i + 1; j < d; ++j) cs = cs + Ri[j] * (double)Z[(size_t)j * ldz + p];
+        const double mu = (a.cp[i] - cs) / a.rii[i];
+        const double t = ((double)Z[(size_t)i * ldz + p] - mu) / a.sig_ref[i];
+        lp += -0.5 * (t * t);
+        lp -= a.lterm[i];
+    }
+    out[p] = lp;
+}
+
+// ------------------------------------------------------------ IMHK accept
+// One lane per chain; proposals of step t for chain c live at p = t*nc + c.
+// sel[c*n_keep + k] = proposal index of the state retained after step
+// (k+1)*thin (-1 = the carried-in state); cnt[p] / cnt_carry[c] count the
+// retained steps spent in each state (moments), final_sel[c] = last state.
+__global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.nc) return;
+    double lw_x = a.lw_state[c];
+    int64_t cur = -1;
+    int64_t acc = 0;
+    int64_t keep = 0;
+    int32_t carry = 0;
+    const uint32_t chain = a.chain0 + (uint32_t)c;
+    for (int64_t t = 0; t < a.T; ++t) {
+        const int64_t p = t * a.nc + c;
+        const double lw_y = a.LW[p];
+        double ratio;
+        if (lw_x == -INFINITY) {
+            ratio = 1.0;
+        } else {
+            const double r = exp(lw_y - lw_x);
+            ratio = r < 1.0 ? r : 1.0;  // min(1.0, r); NaN -> 1.0 like Python's min
+        }
+        const double u = accept_uniform(a.seed, a.step0 + (uint32_t)t, chain);
+        if (u < ratio) {
+            cur = p;
+            lw_x = lw_y;
+            ++acc;
+        }
+        if ((t + 1) % a.thin == 0) {
+            if (a.sel) a.sel[c * a.n_keep + keep] = cur;
+            if (a.cnt) {
+                if (cur < 0)
+                    ++carry;
+                else
+                    a.cnt[cur] += 1;
+            }
+            ++keep;
+        }
+    }
+    a.lw_state[c] = lw_x;
+    a.accepts[c] += acc;
+    a.final_sel[c] = cur;
+    if (a.cnt_carry) a.cnt_carry[c] = carry;
+}
+
+// ------------------------------------------------------------ moments
+// mom[i] += sum_p cnt[p] z[i][p], mom[d+i] += sum_p cnt[p] z[i][p]^2 (int64, exact).
+template <typename ZT>
+__global__ __launch_bounds__(256) void moments_kernel(const ZT* __restrict__ Z, int64_t ldz,
+                                                      const int32_t* __restrict__ cnt, int64_t n,
+                                                      int d, int64_t chunk,
+                                                      unsigned long long* mom) {
+    const int i = blockIdx.y;
+    const int64_t p0 = (int64_t)blockIdx.x * chunk;
+    const int64_t p1 = p0 + chunk < n ? p0 + chunk : n;
+    long long s1 = 0, s2 = 0;
+    for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+        const long long w = cnt ? cnt[p] : 1;
+        const long long z = (long long)Z[(size_t)i * ldz + p];
+        s1 += w * z;
+        s2 += w * z * z;
+    }
+    __shared__ long long r1[256], r2[256];
+    r1[threadIdx.x] = s1;
+    r2[threadIdx.x] = s2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            r1[threadIdx.x] += r1[threadIdx.x + o];
+            r2[threadIdx.x] += r2[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd(mom + i, (unsigned long long)r1[0]);
+        atomicAdd(mom + d + i, (unsigned long long)r2[0]);
+    }
+}
+
+// Carried-in states (row-major or coordinate-major z_state) weighted by cnt_carry.
+template <typename ZT>
+__global__ __launch_bounds__(256) void moments_carry_kernel(const ZT* __restrict__ zs,
+                                                            int coord_major, int64_t nc, int d,
+                                                            const int32_t* __restrict__ cc,
+                                                            unsigned long long* mom) {
+    const int i = blockIdx.x;
+    long long s1 = 0, s2 = 0;
+    for (int64_t c = threadIdx.x; c < nc; c += blockDim.x) {
+        const long long w = cc[c];
+        if (!w) continue;
+        const long long z = (long long)(coord_major ? zs[(size_t)i * nc + c] : zs[(size_t)c * d + i]);
+        s1 += w * z;
+        s2 += w * z * z;
+    }
+    __shared__ long long r1[256], r2[256];
+    r1[threadIdx.x] = s1;
+    r2[threadIdx.x] = s2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            r1[threadIdx.x] += r1[threadIdx.x + o];
+            r2[threadIdx.x] += r2[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd(mom + i, (unsigned long long)r1[0]);
+        atomicAdd(mom + d + i, (unsigned long long)r2[0]);
+    }
+}
+
+// ------------------------------------------------------------ gathers
+// Retained / final states: out row q (d coefficients) = src column sel[q] of Z,
+// or row q of the carried state zs when sel[q] < 0.  Thread per (i, q), q fastest.
+template <typename ZT, typename OT>
+__global__ __launch_bounds__(256) void gather_z_kernel(const ZT* __restrict__ Z, int64_t ldz,
+                                                       const int64_t* __restrict__ sel,
+                                                       int64_t nq, int64_t q_per_chain,
+                                                       const OT* __restrict__ zs,
+                                                       int zs_coord_major, int64_t nc, int d,
+                                                       OT* __restrict__ out, int out_coord_major) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    if (q >= nq) return;
+    const int64_t s = sel[q];
+    OT v;
+    if (s >= 0) {
+        v = (OT)Z[(size_t)i * ldz + s];
+    } else {
+        const int64_t c = q / q_per_chain;
+        v = zs_coord_major ? zs[(size_t)i * nc + c] : zs[(size_t)c * d + i];
+    }
+    if (out_coord_major)
+        out[(size_t)i * nq + q] = v;
+    else
+        out[(size_t)q * d + i] = v;
+}
+
+// Copy rows of V (proposal lattice points, row-major [p][d]) selected by sel;
+// sel < 0 takes the carried state's row from vs (n_chains x d).
+__global__ __launch_bounds__(256) void gather_v_kernel(const double* __restrict__ V,
+                                                       const int64_t* __restrict__ sel,
+                                                       int64_t nq, int64_t q_per_chain,
+                                                       const double* __restrict__ vs, int d,
+                                                       double* __restrict__ out) {
+    const int64_t q = blockIdx.y;
+    const int64_t s = sel[q];
+    const double* src = s >= 0 ? V + (size_t)s * d : vs + (size_t)(q / q_per_chain) * d;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < d; i += gridDim.x * blockDim.x)
+        out[(size_t)q * d + i] = src[i];
+}
+
+// Z[coord][p] (ld ldz) -> out[p][coord] (row-major n x d), 64x64 tiles via LDS.
+template <typename ZT, typename OT>
+__global__ __launch_bounds__(256) void transpose_kernel(const ZT* __restrict__ Z, int64_t ldz,
+                                                        int64_t n, int d, OT* __restrict__ out) {
+    __shared__ OT tile[64][65];
+    const int64_t p0 = (int64_t)blockIdx.x * 64;
+    const int i0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int i = i0 + r;
+        const int64_t p = p0 + tx;
+        if (i < d && p < n) tile[r][tx] = (OT)Z[(size_t)i * ldz + p];
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t p = p0 + r;
+        const int i = i0 + tx;
+        if (i < d && p < n) out[(size_t)p * d + i] = tile[tx][r];
+    }
+}
+
+// Row-major int z (n x d) -> coordinate-major Z[coord][p] (ld ldz).
+template <typename ZT, typename IT>
+__global__ __launch_bounds__(256) void to_coord_major_kernel(const IT* __restrict__ in, int64_t n,
+                                                             int d, ZT* __restrict__ Z,
+                                                             int64_t ldz) {
+    __shared__ ZT tile[64][65];
+    const int64_t p0 = (int64_t)blockIdx.x * 64;
+    const int i0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int64_t p = p0 + r;
+        const int i = i0 + tx;
+        if (i < d && p < n) tile[r][tx] = (ZT)in[(size_t)p * d + i];
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int i = i0 + r;
+        const int64_t p = p0 + tx;
+        if (i < d && p < n) Z[(size_t)i * ldz + p] = tile[tx][r];
+    }
+}
+
+// ------------------------------------------------------------ B z (fp64 MFMA)
+// V[s][r] = sum_c B[r][c] Z[c][s] for s in [0, n), r in [0, d).
+// Block tile 64 samples x 64 coords, 4 waves in 2x2, each wave 2x2 MFMA tiles of
+// v_mfma_f64_16x16x4_f64 (A: lane l -> A[l&15][l>>4]; B: B[l>>4][l&15];
+// D: row (l>>4)+4*reg, col l&15).  K staged through LDS in chunks of 16.
+// Exact (bit-identical to any summation order) when B and z are integers and
+// |partial sums| < 2^53.
+typedef double d4_t __attribute__((ext_vector_type(4)));
+
+template <typename ZT>
+__global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, int64_t ldz,
+                                                      const double* __restrict__ BT, int d,
+                                                      int64_t n, double* __restrict__ V,
+                                                      int64_t ldv) {
+    constexpr int BM = 64, BN = 64, KC = 16, LDP = 80;  // LDP: padded row (doubles)
+    __shared__ double As[KC][LDP];
+    __shared__ double Bs[KC][LDP];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int64_t s0 = (int64_t)blockIdx.x * BM;
+    const int r0 = blockIdx.y * BN;
+    d4_t acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = (d4_t){0.0, 0.0, 0.0, 0.0};
+    for (int c0 = 0; c0 < d; c0 += KC) {
+#pragma unroll
+        for (int e = 0; e < (KC * BM) / 256; ++e) {
+            const int idx = tid + 256 * e;
+            const int kk = idx / BM, m = idx % BM;
+            const int c = c0 + kk;
+            const int64_t s = s0 + m;
+            As[kk][m] = (c < d && s < n) ? (double)Z[(size_t)c * ldz + s] : 0.0;
+            const int r = r0 + m;
+            Bs[kk][m] = (c < d && r < d) ? BT[(size_t)c * d + r] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k4 = 0; k4 < KC; k4 += 4) {
+            const int kk = k4 + (lane >> 4);
+            double af[2], bf[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                af[t] = As[kk][wm * 32 + t * 16 + (lane & 15)];
+                bf[t] = Bs[kk][wn * 32 + t * 16 + (lane & 15)];
+            }
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int64_t s = s0 + wm * 32 + a * 16 + (lane >> 4) + 4 * reg;
+                const int r = r0 + wn * 32 + b * 16 + (lane & 15);
+                if (s < n && r < d) V[(size_t)s * ldv + r] = acc[a][b][reg];
+            }
+}
+
+// ============================================================ launchers
+namespace launch {
+
+template <typename ZT>
+static hipError_t klein_t(const KleinArgs& a, const double* R, const double* RP, const double* RC,
+                          int panel, bool exact, bool wl, void* Z, hipStream_t st) {
+    const dim3 block(256);
+    const dim3 grid((unsigned)((a.n + 255) / 256));
+    ZT* z = (ZT*)Z;
+    if (exact) {
+        if (wl)
+            hipLaunchKernelGGL((klein_exact_kernel<ZT, true>), grid, block, 0, st, a, R, z);
+        else
+            hipLaunchKernelGGL((klein_exact_kernel<ZT, false>), grid, block, 0, st, a, R, z);
+    } else if (panel == 16) {
+        if (wl)
+            hipLaunchKernelGGL((klein_panel_kernel<ZT, 16, true>), grid, block, 0, st, a, RP, RC, z);
+        else
+            hipLaunchKernelGGL((klein_panel_kernel<ZT, 16, false>), grid, block, 0, st, a, RP, RC, z);
+    } else {
+        if (wl)
+            hipLaunchKernelGGL((klein_panel_kernel<ZT, 32, true>), grid, block, 0, st, a, RP, RC, z);
+        else
+            hipLaunchKernelGGL((klein_panel_kernel<ZT, 32, false>), grid, block, 0, st, a, RP, RC, z);
+    }
+    return hipGetLastError();
+}
+
+hipError_t klein(const KleinArgs& a, const double* R, const double* RP, const double* RC,
+                 int panel, bool exact, bool wl, bool z64, void* Z, hipStream_t st) {
+    if (a.n <= 0) return hipSuccess;
+    return z64 ? klein_t<int64_t>(a, R, RP, RC, panel, exact, wl, Z, st)
+               : klein_t<int32_t>(a, R, RP, RC, panel, exact, wl, Z, st);
+}
+
+hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, bool z64, double* out,
+                       hipStream_t st) {
+    if (a.n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((a.n + 255) / 256));
+    if (z64)
+        hipLaunchKernelGGL(log_density_kernel<int64_t>, grid, dim3(256), 0, st, a, R, (const int64_t*)Z, out);
+    else
+        hipLaunchKernelGGL(log_density_kernel<int32_t>, grid, dim3(256), 0, st, a, R, (const int32_t*)Z, out);
+    return hipGetLastError();
+}
+
+hipError_t accept(const AcceptArgs& a, hipStream_t st) {
+    if (a.nc <= 0) return hipSuccess;
+    hipLaunchKernelGGL(imhk_accept_kernel, dim3((unsigned)((a.nc + 255) / 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t moments(const void* Z, bool z64, int64_t ldz, const int32_t* cnt, int64_t n, int d,
+                   unsigned long long* mom, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t chunk = 16384;
+    const dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
+    if (z64)
+        hipLaunchKernelGGL(moments_kernel<int64_t>, grid, dim3(256), 0, st, (const int64_t*)Z, ldz, cnt, n, d, chunk, mom);
+    else
+        hipLaunchKernelGGL(moments_kernel<int32_t>, grid, dim3(256), 0, st, (const int32_t*)Z, ldz, cnt, n, d, chunk, mom);
+    return hipGetLastError();
+}
+
+hipError_t moments_carry(const void* zs, bool z64, int coord_major, int64_t nc, int d,
+                         const int32_t* cc, unsigned long long* mom, hipStream_t st) {
+    if (nc <= 0) return hipSuccess;
+    if (z64)
+        hipLaunchKernelGGL(moments_carry_kernel<int64_t>, dim3(d), dim3(256), 0, st, (const int64_t*)zs, coord_major, nc, d, cc, mom);
+    else
+        hipLaunchKernelGGL(moments_carry_kernel<int32_t>, dim3(d), dim3(256), 0, st, (const int32_t*)zs, coord_major, nc, d, cc, mom);
+    return hipGetLastError();
+}
+
+hipError_t gather_z(const void* Z, bool z64, int64_t ldz, const int64_t* sel, int64_t nq,
+                    int64_t q_per_chain, const void* zs, int zs_coord_major, int64_t nc, int d,
+                    void* out, int out_coord_major, hipStream_t st) {
+    if (nq <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((nq + 255) / 256), (unsigned)d);
+    if (z64)
+        hipLaunchKernelGGL((gather_z_kernel<int64_t, int64_t>), grid, dim3(256), 0, st, (const int64_t*)Z, ldz, sel, nq, q_per_chain, (const int64_t*)zs, zs_coord_major, nc, d, (int64_t*)out, out_coord_major);
+    else
+        hipLaunchKernelGGL((gather_z_kernel<int32_t, int32_t>), grid, dim3(256), 0, st, (const int32_t*)Z, ldz, sel, nq, q_per_chain, (const int32_t*)zs, zs_coord_major, nc, d, (int32_t*)out, out_coord_major);
+    return hipGetLastError();
+}
+
+hipError_t gather_v(const double* V, const int64_t* sel, int64_t nq, int64_t q_per_chain,
+                    const double* vs, int d, double* out, hipStream_t st) {
+    if (nq <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((d + 255) / 256 < 4 ? (d + 255) / 256 : 4), (unsigned)nq);
+    hipLaunchKernelGGL(gather_v_kernel, grid, dim3(256), 0, st, V, sel, nq, q_per_chain, vs, d, out);
+    return hipGetLastError();
+}
+
+hipError_t transpose_out(const void* Z, bool z64, int64_t ldz, int64_t n, int d, void* out,
+                         bool out64, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
+    if (z64 && out64)
+        hipLaunchKernelGGL((transpose_kernel<int64_t, int64_t>), grid, dim3(256), 0, st, (const int64_t*)Z, ldz, n, d, (int64_t*)out);
+    else if (!z64 && out64)
+        hipLaunchKernelGGL((transpose_kernel<int32_t, int64_t>), grid, dim3(256), 0, st, (const int32_t*)Z, ldz, n, d, (int64_t*)out);
+    else if (!z64 && !out64)
+        hipLaunchKernelGGL((transpose_kernel<int32_t, int32_t>), grid, dim3(256), 0, st, (const int32_t*)Z, ldz, n, d, (int32_t*)out);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t to_coord_major(const void* in, bool in64, int64_t n, int d, void* Z, bool z64,
+                          int64_t ldz, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
+    if (z64 && in64)
+        hipLaunchKernelGGL((to_coord_major_kernel<int64_t, int64_t>), grid, dim3(256), 0, st, (const int64_t*)in, n, d, (int64_t*)Z, ldz);
+    else if (!z64 && !in64)
+        hipLaunchKernelGGL((to_coord_major_kernel<int32_t, int32_t>), grid, dim3(256), 0, st, (const int32_t*)in, n, d, (int32_t*)Z, ldz);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t bz(const void* Z, bool z64, int64_t ldz, const double* BT, int d, int64_t n, double* V,
+              int64_t ldv, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
+    if (z64)
+        hipLaunchKernelGGL(bz_gemm_kernel<int64_t>, grid, dim3(256), 0, st, (const int64_t*)Z, ldz, BT, d, n, V, ldv);
+    else
+        hipLaunchKernelGGL(bz_gemm_kernel<int32_t>, grid, dim3(256), 0, st, (const int32_t*)Z, ldz, BT, d, n, V, ldv);
+    return hipGetLastError();
+}
+
+}  // namespace launch
+}  // namespace lgs

@@ -1,0 +1,216 @@
+"""ctypes binding of the HIP C-ABI (``include/lgs.h`` -> ``lgs_amd/_lib/liblgs_hip.so``).
+
+This is the only way the package computes anything: there is no CPU fallback.
+If the library is missing, or no HIP device is visible, constructing a
+``Context`` raises ``LgsError`` immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "liblgs_hip.so")
+
+LGS_OK = 0
+LGS_ERR_INVALID = -1
+LGS_ERR_HIP = -2
+LGS_ERR_NOMEM = -3
+LGS_ERR_OVERFLOW = -4
+LGS_ERR_NONFINITE = -5
+LGS_ERR_STATE = -6
+
+LGS_BASIS_LINEAR_PROBS = 0x1
+LGS_DEVICE_PTRS = 0x1
+LGS_EXACT_ORDER = 0x2
+LGS_WANG_LING = 0x4
+LGS_Z64 = 0x8
+LGS_COORD_MAJOR = 0x10
+
+KERNEL_KLEIN, KERNEL_BZ, KERNEL_ACCEPT, KERNEL_MOMENTS = 0, 1, 2, 3
+
+# every symbol include/lgs.h declares (checked by tests/test_capi_symbols.py)
+EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_destroy", "lgs_set_stream",
+           "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_lattice_points", "lgs_log_density", "lgs_timing_enable",
+           "lgs_timing_get", "lgs_device_info")
+
+
+class LgsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"lgs error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_vp = ctypes.c_void_p
+_dp = ctypes.POINTER(ctypes.c_double)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+
+
+def load_library(path: str = LIB_PATH):
+    """Load liblgs_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise LgsError(LGS_ERR_STATE, f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(path)
+    L.lgs_version.restype = ctypes.c_int
+    L.lgs_last_error.restype = ctypes.c_char_p
+    L.lgs_create.argtypes = [ctypes.POINTER(_vp), ctypes.c_int]
+    L.lgs_destroy.argtypes = [_vp]
+    L.lgs_set_stream.argtypes = [_vp, _vp]
+    L.lgs_set_basis.argtypes = [_vp, ctypes.c_int64, _dp, _dp, _dp, ctypes.c_double, ctypes.c_int32,
+                                ctypes.c_uint32]
+    L.lgs_klein.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, _vp, _vp, _vp,
+                            ctypes.c_uint32]
+    L.lgs_imhk.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint64,
+                           ctypes.c_int64, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                           ctypes.c_uint32]
+    L.lgs_lattice_points.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint32]
+    L.lgs_log_density.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint32]
+    L.lgs_timing_enable.argtypes = [_vp, ctypes.c_int]
+    L.lgs_timing_get.argtypes = [_vp, ctypes.c_int, _dp, _i64p]
+    L.lgs_device_info.argtypes = [_vp, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                  _i64p]
+    for name in EXPORTS:
+        if name not in ("lgs_version", "lgs_last_error"):
+            getattr(L, name).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != LGS_OK:
+        msg = _lib.lgs_last_error().decode(errors="replace")
+        raise LgsError(rc, msg)
+
+
+def _ptr(a):
+    """Host numpy array or device tensor (anything with data_ptr()) -> void*."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        if not a.flags.c_contiguous:
+            raise ValueError("arrays must be C-contiguous")
+        return ctypes.c_void_p(a.ctypes.data)
+    if hasattr(a, "data_ptr"):
+        return ctypes.c_void_p(a.data_ptr())
+    if isinstance(a, int):
+        return ctypes.c_void_p(a)
+    raise TypeError(f"unsupported buffer {type(a)}")
+
+
+class Context:
+    """One HIP device context (stream + device-resident basis + scratch)."""
+
+    def __init__(self, device: int = 0):
+        L = load_library()
+        h = _vp()
+        _check(L.lgs_create(ctypes.byref(h), int(device)))
+        self._h = h
+        self.device = device
+        self.d = 0
+
+    def close(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.lgs_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    # ---------------------------------------------------------------- setup
+    def set_stream(self, stream_handle):
+        _check(_lib.lgs_set_stream(self._h, _vp(stream_handle) if stream_handle else None))
+
+    def set_basis(self, R, cprime, B, sigma, precision=10, linear_probs=False):
+        R = np.ascontiguousarray(R, dtype=np.float64)
+        cp = np.ascontiguousarray(cprime, dtype=np.float64)
+        Bc = None if B is None else np.ascontiguousarray(B, dtype=np.float64)
+        d = R.shape[0]
+        if R.shape != (d, d) or cp.shape != (d,) or (Bc is not None and Bc.shape != (d, d)):
+            raise ValueError("shape mismatch between R, cprime and B")
+        flags = LGS_BASIS_LINEAR_PROBS if linear_probs else 0
+        _check(_lib.lgs_set_basis(self._h, d, R.ctypes.data_as(_dp), cp.ctypes.data_as(_dp),
+                                  None if Bc is None else Bc.ctypes.data_as(_dp), float(sigma),
+                                  int(precision), flags))
+        self.d = d
+        self._keep = (R, cp, Bc)
+
+    # ---------------------------------------------------------------- compute
+    def klein(self, seed, first, n, z_out=None, v_out=None, logw_out=None, flags=0):
+        """Raw lgs_klein on caller-provided buffers (numpy host or device tensors)."""
+        _check(_lib.lgs_klein(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(first), int(n),
+                              _ptr(z_out), _ptr(v_out), _ptr(logw_out), int(flags)))
+
+    def klein_host(self, seed, first, n, *, want_z=True, want_v=True, want_logw=False, flags=0):
+        """Klein samples into fresh host arrays; int32 first, int64 on overflow."""
+        d = self.d
+        for z64 in (False, True):
+            f = flags | (LGS_Z64 if z64 else 0)
+            z = np.empty((n, d), dtype=np.int64 if z64 else np.int32) if want_z else None
+            v = np.empty((n, d)) if want_v else None
+            lw = np.empty(n) if want_logw else None
+            try:
+                self.klein(seed, first, n, z, v, lw, f)
+            except LgsError as e:
+                if e.code == LGS_ERR_OVERFLOW and not z64:
+                    continue
+                raise
+            return {"z": None if z is None else z.astype(np.int64, copy=False), "v": v, "logw": lw}
+        raise AssertionError("unreachable")
+
+    def imhk(self, seed, first_chain, n_chains, first_step, n_steps, thin, z_state, logw_state,
+             state_init, accepts, z_samples=None, v_samples=None, moments=None, flags=0):
+        _check(_lib.lgs_imhk(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(first_chain),
+                             int(n_chains), int(first_step), int(n_steps), int(thin),
+                             _ptr(z_state), _ptr(logw_state), _ptr(state_init), _ptr(accepts),
+                             _ptr(z_samples), _ptr(v_samples), _ptr(moments), int(flags)))
+
+    def lattice_points(self, z, v_out=None, flags=0):
+        if isinstance(z, np.ndarray):
+            z64 = z.dtype == np.int64
+            zz = np.ascontiguousarray(z, dtype=np.int64 if z64 else np.int32)
+            n = zz.shape[0]
+            v = np.empty((n, self.d)) if v_out is None else v_out
+            _check(_lib.lgs_lattice_points(self._h, n, _ptr(zz), _ptr(v),
+                                           int(flags | (LGS_Z64 if z64 else 0))))
+            return v
+        n = z.shape[0] if not (flags & LGS_COORD_MAJOR) else z.shape[1]
+        _check(_lib.lgs_lattice_points(self._h, n, _ptr(z), _ptr(v_out), int(flags)))
+        return v_out
+
+    def log_density(self, z):
+        zz = np.ascontiguousarray(z)
+        z64 = zz.dtype == np.int64
+        if not z64:
+            zz = zz.astype(np.int32)
+        out = np.empty(zz.shape[0])
+        _check(_lib.lgs_log_density(self._h, zz.shape[0], _ptr(zz), _ptr(out),
+                                    LGS_Z64 if z64 else 0))
+        return out
+
+    # ---------------------------------------------------------------- timing / info
+    def timing_enable(self, on=True):
+        _check(_lib.lgs_timing_enable(self._h, 1 if on else 0))
+
+    def timing_get(self, kernel):
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int64(0)
+        _check(_lib.lgs_timing_get(self._h, int(kernel), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def device_info(self):
+        buf = ctypes.create_string_buffer(256)
+        ncu = ctypes.c_int(0)
+        mem = ctypes.c_int64(0)
+        _check(_lib.lgs_device_info(self._h, buf, 256, ctypes.byref(ncu), ctypes.byref(mem)))
+        return {"name": buf.value.decode(), "n_cu": ncu.value, "hbm_bytes": mem.value}
+
+
+def version() -> int:
+    return load_library().lgs_version()

@@ -69,6 +69,11 @@ def lib():
         L.lgso_klein_parallel.argtypes = [ctypes.c_int64, _dp, _dp, ctypes.c_double, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                                           ctypes.c_int64, _i64p, ctypes.c_int]
+        L.lgso_imhk_parallel.restype = ctypes.c_int
+        L.lgso_imhk_parallel.argtypes = [ctypes.c_int64, _dp, _dp, _dp, _dp, ctypes.c_double,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                         ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint64,
+                                         ctypes.c_int64, _i64p, _dp, _i32p, _i64p, ctypes.c_int]
         L.lgso_log_weight.restype = ctypes.c_double
         L.lgso_log_weight.argtypes = [ctypes.c_int64, _dp, _dp, _dp, _dp, ctypes.c_double,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, _i64p]
@@ -224,3 +229,24 @@ def imhk(R, cprime, B, sigma, n_chains, n_steps, *, center=None, seed=0, first_c
         raise RuntimeError(f"lgso_imhk failed rc={rc}")
     state["trace"] = ztr
     return state
+
+
+def imhk_parallel(R, cprime, B, sigma, n_chains, n_steps, *, center=None, seed=0, first_chain=0,
+                  first_step=1, mode=IMHK_REFERENCE, precision=10, use_log_space=True, threads=1):
+    """Philox-mode IMHK chains in parallel (OpenMP); returns (z_state, lw, accepts)."""
+    R = np.ascontiguousarray(R, dtype=np.float64)
+    cp = np.ascontiguousarray(cprime, dtype=np.float64)
+    Bc = np.ascontiguousarray(B, dtype=np.float64)
+    c = None if center is None else np.ascontiguousarray(center, dtype=np.float64)
+    d = R.shape[0]
+    z = np.zeros((n_chains, d), dtype=np.int64)
+    lw = np.zeros(n_chains)
+    init = np.zeros(n_chains, dtype=np.int32)
+    acc = np.zeros(n_chains, dtype=np.int64)
+    rc = lib().lgso_imhk_parallel(d, _p(R, _dp), _p(cp, _dp), _p(Bc, _dp), _p(c, _dp), sigma,
+                                  precision, int(use_log_space), mode, seed, first_chain, n_chains,
+                                  first_step, n_steps, _p(z, _i64p), _p(lw, _dp), _p(init, _i32p),
+                                  _p(acc, _i64p), threads)
+    if rc != 0:
+        raise RuntimeError(f"lgso_imhk_parallel failed rc={rc}")
+    return z, lw, acc

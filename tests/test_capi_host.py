@@ -1,0 +1,109 @@
+"""CPU-side checks of the boundary: the C-ABI library loads and exports every
+entry point include/lgs.h declares; host-side logic of the drop-in that needs
+no device (validation, lattice builders, counters)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "lgs.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(lgs_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_declares_the_abi():
+    syms = declared_symbols()
+    for s in ("lgs_create", "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_last_error"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from lgs_amd import _capi
+    L = _capi.load_library()
+    for s in declared_symbols():
+        assert hasattr(L, s), f"{s} declared in lgs.h but not exported"
+        assert s in _capi.EXPORTS, f"{s} not bound in _capi.EXPORTS"
+    assert set(_capi.EXPORTS) == set(declared_symbols())
+    assert L.lgs_version() == 100
+
+
+def test_library_is_gfx950_code_object():
+    from lgs_amd import _capi
+    blob = open(_capi.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_no_device_fails_loudly():
+    import torch
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a device is visible")
+    from lgs_amd import _capi
+    with pytest.raises(_capi.LgsError):
+        _capi.Context(0)
+
+
+def test_sampler_argument_validation_before_device():
+    from lgs_amd.lattices import SimpleLattice
+    from lgs_amd.samplers import IMHKSampler, KleinSampler
+    lat = SimpleLattice(np.eye(3))
+    with pytest.raises(ValueError):
+        KleinSampler(lat, 0.0)
+    with pytest.raises(ValueError):
+        KleinSampler(lat, -1.0)
+    with pytest.raises(ValueError):
+        KleinSampler(lat, 1.0, center=[0.0, 1.0])
+    with pytest.raises(ValueError):
+        IMHKSampler(lat, -2.0)
+
+
+def test_burn_in_overflow_like_reference():
+    """imhk.py:82-88 raises OverflowError for large d; the drop-in keeps that."""
+    from lgs_amd.lattices import build_config
+    from lgs_amd.samplers.imhk import IMHKSampler
+
+    class Fake:
+        pass
+    lat, sigma = build_config("C3_ntru512")
+    f = Fake()
+    f.dimension, f.sigma, f.lattice = lat.dimension, sigma, lat
+    with pytest.raises(OverflowError):
+        IMHKSampler._estimate_burn_in(f)
+    g = Fake()
+    small = np.eye(4) * 3
+    from lgs_amd.lattices import SimpleLattice
+    g.dimension, g.sigma, g.lattice = 4, 2.0, SimpleLattice(small)
+    assert IMHKSampler._estimate_burn_in(g) == min(2 * int(np.ceil(-np.log(0.01) * 4 * (2 / 3) ** 4)), 10000)
+
+
+def test_lattice_builders_match_reference_constructions():
+    from lgs_amd import lattices
+    B = lattices.ntru_basis(8, 97, seed=3)
+    h = lattices.ntru_public(8, 97, seed=3)
+    n = 8
+    assert np.array_equal(B[:n, :n], 97 * np.eye(n)) and not B[:n, n:].any()
+    assert np.array_equal(B[n:, n:], np.eye(n))
+    for i in range(n):
+        for j in range(n):
+            assert B[n + i, j] == h[(j - i) % n]
+    Q = lattices.qary_basis(4, 6, 31, seed=2)
+    assert Q.shape == (10, 10) and np.array_equal(Q[:4, :4], 31 * np.eye(4))
+    assert np.array_equal(Q[4:, 4:], np.eye(6)) and Q[4:, :4].max() < 31
+    # deterministic across machines: Philox-generated integers
+    assert np.array_equal(lattices.ntru_public(512, 12289, 1), lattices.ntru_public(512, 12289, 1))
+
+
+def test_simple_lattice_duck_type():
+    from lgs_amd.lattices import SimpleLattice
+    B = np.array([[4.0, 1.0], [1.0, 3.0]])
+    lat = SimpleLattice(B)
+    assert lat.dimension == 2 and lat.basis is lat.get_basis()
+    # row Gram-Schmidt: |b1| = sqrt(17), |b2*| = det / |b1|
+    assert lat.min_gram_schmidt_norm == pytest.approx(min(np.sqrt(17), 11 / np.sqrt(17)))
+    assert lat.smoothing_parameter() > 0

@@ -1,0 +1,270 @@
+"""HIP path vs the oracle and the reference's golden vectors (needs an MI355X).
+
+Integer outputs (coefficients z, accept decisions, moments) must be bit-exact;
+lattice points v = B z are exact for integer bases (all partial sums are
+integers < 2^53) and within rtol 1e-12 otherwise.  Both device samplers are
+checked: LGS_EXACT_ORDER (the reference's sequential fp64 order) and the
+default blocked panel kernel.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden_R, klein_goldens, load_golden
+
+pytestmark = pytest.mark.gpu
+
+MODES = {"exact": 2, "panel": 0}  # LGS_EXACT_ORDER = 0x2
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from lgs_amd import _capi
+    return _capi
+
+
+@pytest.fixture(scope="module")
+def ctx(capi):
+    return capi.Context(0)
+
+
+def _is_int(B):
+    return B is not None and np.array_equal(B, np.round(B))
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("name", klein_goldens())
+def test_klein_matches_reference_goldens(ctx, name, mode):
+    g = load_golden(name)
+    R, cp, B = golden_R(g)
+    ctx.set_basis(R, cp, B, float(g["sigma"]))
+    r = ctx.klein_host(int(g["seed"]), int(g["first_sample"]), int(g["n"]), want_z=True,
+                       want_v=True, flags=MODES[mode])
+    mism = ~(r["z"] == g["z"]).all(1)
+    assert mism.sum() == 0, f"{mism.sum()} of {len(mism)} samples differ"
+    if "v" in g:
+        if _is_int(B):
+            assert np.array_equal(r["v"], g["v"])
+        else:
+            np.testing.assert_allclose(r["v"], g["v"], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("case", ["ntru128", "qary128", "gauss16", "Z64", "B2_center"])
+def test_klein_matches_oracle_seeded(ctx, oracle, case, mode):
+    g = load_golden(f"klein_{case}.npz")
+    R, cp, B = golden_R(g)
+    sigma = float(g["sigma"])
+    seed, first, n = 0xC0FFEE + len(case), 12345, 1536
+    ctx.set_basis(R, cp, B, sigma)
+    r = ctx.klein_host(seed, first, n, want_z=True, want_v=True, flags=MODES[mode])
+    o = oracle.klein(R, cp, sigma, n, seed=seed, first_sample=first, B=B)
+    assert np.array_equal(r["z"], o["z"])
+    if _is_int(B):
+        assert np.array_equal(r["v"], o["v"])
+    else:
+        np.testing.assert_allclose(r["v"], o["v"], rtol=1e-12, atol=1e-9)
+
+
+def test_klein_full_size_ntru1024_vs_oracle(ctx, oracle):
+    """BASELINE config C3 basis (d = 1024): device vs oracle on 64 samples, both kernels."""
+    from lgs_amd.lattices import build_config
+    lat, sigma = build_config("C3_ntru512")
+    R, cp = oracle.qr_prepare(lat.basis)
+    ctx.set_basis(R, cp, lat.basis, sigma)
+    o = oracle.klein(R, cp, sigma, 64, seed=99, first_sample=7, B=lat.basis)
+    for f in MODES.values():
+        r = ctx.klein_host(99, 7, 64, want_z=True, want_v=True, flags=f)
+        assert np.array_equal(r["z"], o["z"])
+        assert np.array_equal(r["v"], o["v"])
+
+
+def test_klein_batch_and_offset_invariance(ctx):
+    g = load_golden("klein_ntru128.npz")
+    R, cp, B = golden_R(g)
+    ctx.set_basis(R, cp, B, float(g["sigma"]))
+    a = ctx.klein_host(5, 0, 3000, want_z=True, want_v=False)["z"]
+    b1 = ctx.klein_host(5, 0, 1234, want_z=True, want_v=False)["z"]
+    b2 = ctx.klein_host(5, 1234, 3000 - 1234, want_z=True, want_v=False)["z"]
+    assert np.array_equal(a, np.vstack([b1, b2]))
+    c = ctx.klein_host(5, 1000, 10, want_z=True, want_v=False)["z"]
+    assert np.array_equal(c, a[1000:1010])
+    d = ctx.klein_host(6, 0, 10, want_z=True, want_v=False)["z"]
+    assert not np.array_equal(d, a[:10])
+
+
+def test_small_launch_chunks_and_panel16(capi, oracle):
+    """Chunked launches (LGS_MAX_PROPOSALS) and the 16-row panel give identical z."""
+    g = load_golden("klein_qary128.npz")
+    R, cp, B = golden_R(g)
+    os.environ["LGS_MAX_PROPOSALS"] = "100"
+    os.environ["LGS_PANEL"] = "16"
+    try:
+        c2 = capi.Context(0)
+        c2.set_basis(R, cp, B, float(g["sigma"]))
+        r = c2.klein_host(int(g["seed"]), 0, int(g["n"]), want_z=True, want_v=True)
+    finally:
+        del os.environ["LGS_MAX_PROPOSALS"], os.environ["LGS_PANEL"]
+    assert np.array_equal(r["z"], g["z"])
+    assert np.array_equal(r["v"], g["v"])
+
+
+def test_overflow_falls_back_to_int64(ctx, capi):
+    g = load_golden("klein_edge6.npz")
+    R, cp, B = golden_R(g)
+    ctx.set_basis(R, cp, B, float(g["sigma"]))
+    z32 = np.empty((4, 6), dtype=np.int32)
+    with pytest.raises(capi.LgsError) as e:
+        ctx.klein(int(g["seed"]), 0, 4, z32, None, None, 0)
+    assert e.value.code == capi.LGS_ERR_OVERFLOW
+    r = ctx.klein_host(int(g["seed"]), 0, int(g["n"]), want_z=True, want_v=True)
+    assert np.array_equal(r["z"], g["z"])
+
+
+def test_device_pointers_coordinate_major(ctx, capi):
+    import torch
+    g = load_golden("klein_ntru32.npz")
+    R, cp, B = golden_R(g)
+    ctx.set_basis(R, cp, B, float(g["sigma"]))
+    n, d = int(g["n"]), R.shape[0]
+    z = torch.empty((d, n), dtype=torch.int32, device="cuda:0")
+    v = torch.empty((n, d), dtype=torch.float64, device="cuda:0")
+    lw = torch.empty((n,), dtype=torch.float64, device="cuda:0")
+    torch.cuda.synchronize()
+    ctx.klein(int(g["seed"]), 0, n, z, v, lw, capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR)
+    assert np.array_equal(z.cpu().numpy().T, g["z"])
+    assert np.array_equal(v.cpu().numpy(), g["v"])
+    zr = torch.empty((n, d), dtype=torch.int32, device="cuda:0")
+    ctx.klein(int(g["seed"]), 0, n, zr, None, None, capi.LGS_DEVICE_PTRS)
+    assert np.array_equal(zr.cpu().numpy(), g["z"])
+
+
+def test_lattice_points_and_log_density(ctx, oracle):
+    g = load_golden("klein_gauss16.npz")
+    R, cp, B = golden_R(g)
+    sigma = float(g["sigma"])
+    ctx.set_basis(R, cp, B, sigma)
+    v = ctx.lattice_points(g["z"].astype(np.int64))
+    np.testing.assert_allclose(v, g["v"], rtol=1e-12, atol=1e-9)
+    lq = ctx.log_density(g["z"][:32])
+    for k in range(32):
+        z = g["z"][k]
+        lw = oracle.log_weight(R, cp, B, sigma, z, center=g["center"])
+        vv = B @ z
+        log_target = -np.dot(vv - g["center"], vv - g["center"]) / (2 * sigma ** 2)
+        assert lq[k] == pytest.approx(log_target - lw, rel=1e-11, abs=1e-9)
+
+
+# ------------------------------------------------------------------ IMHK
+def _imhk_dev(ctx, R, cp, B, sigma, nc, steps, seed, thin=1, flags=0, split=None, moments=False):
+    d = R.shape[0]
+    ctx.set_basis(R, cp, B, sigma)
+    st = dict(z=np.zeros((nc, d), dtype=np.int32), lw=np.zeros(nc), init=np.zeros(nc, dtype=np.int32),
+              acc=np.zeros(nc, dtype=np.int64))
+    mom = np.zeros(2 * d, dtype=np.int64) if moments else None
+    parts = [steps] if split is None else split
+    outs, t = [], 1
+    for s in parts:
+        zs = np.zeros((nc, s // thin, d), dtype=np.int32)
+        ctx.imhk(seed, 0, nc, t, s, thin, st["z"], st["lw"], st["init"], st["acc"], z_samples=zs,
+                 moments=mom, flags=flags)
+        outs.append(zs)
+        t += s
+    return st, np.concatenate(outs, axis=1), mom
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("name", ["imhk_ntru32.npz", "imhk_B2.npz"])
+def test_imhk_matches_reference_goldens(ctx, name, mode):
+    g = load_golden(name)
+    nc, ns, d = g["z"].shape
+    st, trace, _ = _imhk_dev(ctx, g["R"], g["cprime"], g["B"], float(g["sigma"]), nc, ns,
+                             int(g["seed"]), flags=MODES[mode])
+    assert np.array_equal(trace, g["z"])
+    assert np.array_equal(st["acc"], g["accepted"].sum(1))
+    np.testing.assert_allclose(st["lw"], g["log_weight"][:, -1], rtol=1e-10)
+
+
+@pytest.mark.parametrize("wl", [False, True])
+def test_imhk_matches_oracle(ctx, oracle, capi, wl):
+    g = load_golden("klein_ntru32.npz")
+    R, cp, B = golden_R(g)
+    sigma = float(g["sigma"])
+    nc, steps, thin = 8, 48, 3
+    flags = capi.LGS_WANG_LING if wl else 0
+    st, zs, mom = _imhk_dev(ctx, R, cp, B, sigma, nc, steps, 777, thin=thin, flags=flags,
+                            split=[24, 24], moments=True)
+    o = oracle.imhk(R, cp, B, sigma, nc, steps, seed=777, first_step=1,
+                    mode=oracle.IMHK_WANG_LING if wl else oracle.IMHK_REFERENCE, trace=True)
+    kept = o["trace"][:, thin - 1::thin]
+    assert np.array_equal(zs, kept)
+    assert np.array_equal(st["acc"], o["accepts"])
+    assert np.array_equal(st["z"], o["z"])
+    np.testing.assert_allclose(st["lw"], o["lw"], rtol=1e-9)
+    flat = kept.reshape(-1, R.shape[0]).astype(np.int64)
+    assert np.array_equal(mom[: R.shape[0]], flat.sum(0))
+    assert np.array_equal(mom[R.shape[0]:], (flat * flat).sum(0))
+    if not wl:
+        assert st["acc"].sum() == nc * steps  # reference-mode acceptance is exactly 1
+
+
+def test_imhk_block_split_invariance(capi):
+    g = load_golden("klein_ntru128.npz")
+    R, cp, B = golden_R(g)
+    os.environ["LGS_MAX_PROPOSALS"] = "200"
+    try:
+        c2 = capi.Context(0)
+        st_a, zs_a, mom_a = _imhk_dev(c2, R, cp, B, float(g["sigma"]), 16, 40, 31, thin=2,
+                                      flags=capi.LGS_WANG_LING, moments=True)
+    finally:
+        del os.environ["LGS_MAX_PROPOSALS"]
+    c3 = capi.Context(0)
+    st_b, zs_b, mom_b = _imhk_dev(c3, R, cp, B, float(g["sigma"]), 16, 40, 31, thin=2,
+                                  flags=capi.LGS_WANG_LING, split=[10, 30], moments=True)
+    assert np.array_equal(zs_a, zs_b)
+    assert np.array_equal(st_a["acc"], st_b["acc"])
+    assert np.array_equal(mom_a, mom_b)
+
+
+# ------------------------------------------------------------------ drop-in API
+def test_drop_in_klein_sampler(oracle):
+    from lgs_amd.lattices import SimpleLattice
+    from lgs_amd.samplers import KleinSampler
+    B = np.array([[4.0, 1.0], [1.0, 3.0]])
+    s = KleinSampler(SimpleLattice(B), 2.0, seed=11)
+    v = s.sample(2000)
+    assert v.shape == (2000, 2) and s.sample(1).shape == (1, 2) and s.sample_single().shape == (2,)
+    R, cp = oracle.qr_prepare(B)
+    o = oracle.klein(R, cp, 2.0, 2000, seed=11, B=B)
+    assert np.array_equal(v, o["v"])
+    np.random.seed(3)
+    a = KleinSampler(SimpleLattice(B), 2.0).sample(50)
+    np.random.seed(3)
+    b = KleinSampler(SimpleLattice(B), 2.0).sample(50)
+    assert np.array_equal(a, b)
+    # empirical moments (reference test style: mean within 3 sigma / sqrt(N))
+    big = KleinSampler(SimpleLattice(np.eye(8)), 5.0, seed=4).sample(20000)
+    assert np.all(np.abs(big.mean(0)) < 3 * 5 / np.sqrt(20000) * 1.5)
+    np.testing.assert_allclose(np.cov(big.T), 25 * np.eye(8), atol=0.1 * 25)
+    assert np.isfinite(s.compute_log_density(v[0]))
+    assert s.compute_log_density(v[0] + 0.5) == -np.inf
+    info = s.diagnostic_info()
+    assert info["algorithm"] == "Refined Klein"
+
+
+def test_drop_in_imhk_sampler(oracle):
+    from lgs_amd.lattices import SimpleLattice
+    from lgs_amd.samplers import IMHKSampler
+    g = load_golden("imhk_B2.npz")
+    s = IMHKSampler(SimpleLattice(g["B"]), float(g["sigma"]), burn_in=0, seed=int(g["seed"]),
+                    chain_id=0)
+    states = [s.step()[0] for _ in range(5)]
+    rest = s.sample(195)
+    V = np.vstack([np.array(states), rest])
+    ref = (g["B"] @ g["z"][0].T).T
+    assert np.array_equal(V, ref)
+    assert s.accepted_proposals == s.total_proposals == 200
+    assert s.stats.acceptance_rate == 1.0
+    chain = s.run_chain(10, save_every=3)
+    assert len(chain) == 4
