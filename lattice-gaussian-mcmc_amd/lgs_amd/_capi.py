@@ -55,6 +55,15 @@ def load_library(path: str = LIB_PATH):
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: PyTorch ships its own libamdhip64 (soname
+    # libamdhip64.so.7) and binds it by the unversioned name, so it must be
+    # loaded first; liblgs_hip.so's NEEDED libamdhip64.so.7 then resolves to the
+    # same runtime and device pointers / streams are shared with torch.
+    if os.environ.get("LGS_NO_TORCH") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     if not os.path.exists(path):
         raise LgsError(LGS_ERR_STATE, f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
     L = ctypes.CDLL(path)
