@@ -678,6 +678,35 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
     return finish(c);
 }
 
+int lgs_sample_z(lgs_ctx* c, int64_t n, const double* mu, const double* sigma, const double* u,
+                 int32_t precision, int64_t* z_out, double* log_norm_out, uint32_t flags) {
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    if (n < 0 || !mu || !sigma || !u || !z_out) return fail(LGS_ERR_INVALID, "bad arguments");
+    if (n == 0) return LGS_OK;
+    for (int64_t i = 0; i < n; ++i)
+        if (!(sigma[i] > 0) || !std::isfinite(sigma[i]) || !std::isfinite(mu[i]))
+            return fail(LGS_ERR_INVALID, "sigma must be positive/finite and mu finite");
+    DevBuf buf;
+    if ((rc = buf.reserve((size_t)n * 8 * 5))) return rc;
+    double* dmu = buf.as<double>();
+    double* dsig = dmu + n;
+    double* du = dsig + n;
+    int64_t* dz = (int64_t*)(du + n);
+    double* dln = (double*)(dz + n);
+    HIP_TRY(hipMemcpyAsync(dmu, mu, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(dsig, sigma, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(du, u, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(lgs::launch::samplez_probe(dmu, dsig, du, n, precision,
+                                       (flags & LGS_BASIS_LINEAR_PROBS) ? 1 : 0,
+                                       (flags & LGS_SAMPLEZ_TABLE) ? 1 : 0, dz, dln, c->stream));
+    HIP_TRY(hipMemcpyAsync(z_out, dz, n * 8, hipMemcpyDeviceToHost, c->stream));
+    if (log_norm_out)
+        HIP_TRY(hipMemcpyAsync(log_norm_out, dln, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return LGS_OK;
+}
+
 int lgs_timing_enable(lgs_ctx* c, int enable) {
     int rc = check_ctx(c, false);
     if (rc) return rc;

@@ -59,6 +59,9 @@ namespace launch {
 hipError_t klein(const KleinArgs& a, const double* R, const double* RP, const double* RC,
                  int panel, bool exact, bool wl, bool z64, void* Z, hipStream_t st);
 hipError_t accept(const AcceptArgs& a, hipStream_t st);
+hipError_t samplez_probe(const double* mu, const double* sig, const double* u, int64_t n,
+                         int precision, int linear, int force_table, int64_t* z, double* ln,
+                         hipStream_t st);
 hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, bool z64, double* out,
                        hipStream_t st);
 hipError_t moments(const void* Z, bool z64, int64_t ldz, const int32_t* cnt, int64_t n, int d,

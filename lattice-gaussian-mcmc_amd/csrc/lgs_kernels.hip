@@ -50,8 +50,8 @@ __device__ __forceinline__ int64_t decide_coord(const KleinArgs& a, int i, doubl
     if (s == 0.0) {  // sigma_i < 1e-10: round, no draw (klein.py:201-204)
         zi = (int64_t)rint(mu);
     } else {
-        SampleZOut o = sample_z_table(mu, s, a.precision, a.linear_probs != 0,
-                                      rs.u((uint32_t)(a.d - 1 - i)));
+        SampleZOut o = sample_z(mu, s, a.precision, a.linear_probs != 0,
+                                rs.u((uint32_t)(a.d - 1 - i)));
         zi = o.z;
         if (WL) lw += o.log_norm;
     }
@@ -187,6 +187,24 @@ __global__ __launch_bounds__(256) void log_density_kernel(const KleinArgs a,
         lp -= a.lterm[i];
     }
     out[p] = lp;
+}
+
+// ------------------------------------------------------------ SampleZ probe
+// Direct evaluation of the device SampleZ for given (mu, sigma, u) triples
+// (unit test / diagnostics of klein.py:101-179's decision).
+__global__ __launch_bounds__(256) void samplez_probe_kernel(const double* __restrict__ mu,
+                                                            const double* __restrict__ sig,
+                                                            const double* __restrict__ u,
+                                                            int64_t n, int precision,
+                                                            int linear, int force_table,
+                                                            int64_t* __restrict__ z,
+                                                            double* __restrict__ ln) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    SampleZOut o = force_table ? sample_z_table(mu[p], sig[p], precision, linear != 0, u[p])
+                               : sample_z(mu[p], sig[p], precision, linear != 0, u[p]);
+    z[p] = o.z;
+    if (ln) ln[p] = o.log_norm;
 }
 
 // ------------------------------------------------------------ IMHK accept
@@ -497,6 +515,15 @@ hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, bool 
         hipLaunchKernelGGL(log_density_kernel<int64_t>, grid, dim3(256), 0, st, a, R, (const int64_t*)Z, out);
     else
         hipLaunchKernelGGL(log_density_kernel<int32_t>, grid, dim3(256), 0, st, a, R, (const int32_t*)Z, out);
+    return hipGetLastError();
+}
+
+hipError_t samplez_probe(const double* mu, const double* sig, const double* u, int64_t n,
+                         int precision, int linear, int force_table, int64_t* z, double* ln,
+                         hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(samplez_probe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       mu, sig, u, n, precision, linear, force_table, z, ln);
     return hipGetLastError();
 }
 

@@ -28,12 +28,13 @@ LGS_EXACT_ORDER = 0x2
 LGS_WANG_LING = 0x4
 LGS_Z64 = 0x8
 LGS_COORD_MAJOR = 0x10
+LGS_SAMPLEZ_TABLE = 0x20
 
 KERNEL_KLEIN, KERNEL_BZ, KERNEL_ACCEPT, KERNEL_MOMENTS = 0, 1, 2, 3
 
 # every symbol include/lgs.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_destroy", "lgs_set_stream",
-           "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_lattice_points", "lgs_log_density", "lgs_timing_enable",
+           "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_lattice_points", "lgs_log_density", "lgs_sample_z", "lgs_timing_enable",
            "lgs_timing_get", "lgs_device_info")
 
 
@@ -81,6 +82,8 @@ def load_library(path: str = LIB_PATH):
                            ctypes.c_uint32]
     L.lgs_lattice_points.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint32]
     L.lgs_log_density.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint32]
+    L.lgs_sample_z.argtypes = [_vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int32, _vp, _vp,
+                               ctypes.c_uint32]
     L.lgs_timing_enable.argtypes = [_vp, ctypes.c_int]
     L.lgs_timing_get.argtypes = [_vp, ctypes.c_int, _dp, _i64p]
     L.lgs_device_info.argtypes = [_vp, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
@@ -202,6 +205,17 @@ class Context:
         _check(_lib.lgs_log_density(self._h, zz.shape[0], _ptr(zz), _ptr(out),
                                     LGS_Z64 if z64 else 0))
         return out
+
+    def sample_z(self, mu, sigma, u, precision=10, table=False, linear_probs=False):
+        mu = np.ascontiguousarray(mu, dtype=np.float64)
+        sg = np.ascontiguousarray(np.broadcast_to(sigma, mu.shape), dtype=np.float64)
+        uu = np.ascontiguousarray(u, dtype=np.float64)
+        z = np.empty(mu.shape, dtype=np.int64)
+        ln = np.empty(mu.shape)
+        f = (LGS_SAMPLEZ_TABLE if table else 0) | (LGS_BASIS_LINEAR_PROBS if linear_probs else 0)
+        _check(_lib.lgs_sample_z(self._h, mu.size, _ptr(mu), _ptr(sg), _ptr(uu), int(precision),
+                                 _ptr(z), _ptr(ln), f))
+        return z, ln
 
     # ---------------------------------------------------------------- timing / info
     def timing_enable(self, on=True):

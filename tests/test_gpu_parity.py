@@ -268,3 +268,31 @@ def test_drop_in_imhk_sampler(oracle):
     assert s.stats.acceptance_rate == 1.0
     chain = s.run_chain(10, save_every=3)
     assert len(chain) == 4
+
+
+# ------------------------------------------------------------------ SampleZ unit tests
+@pytest.mark.parametrize("table", [False, True])
+def test_samplez_reference_decision_table(ctx, table):
+    """Device SampleZ (Euler-Maclaurin path and table walk) vs the reference's own
+    decisions over 13 sigma regimes (tests/golden/samplez_table.npz)."""
+    g = load_golden("samplez_table.npz")
+    z, ln = ctx.sample_z(g["mu"], g["sigma"], g["u"], table=table)
+    assert np.array_equal(z, g["z"])
+
+
+def test_samplez_em_vs_table_vs_oracle_stress(ctx, oracle):
+    rng = np.random.default_rng(123)
+    n = 20000
+    sig = np.exp(rng.uniform(np.log(0.005), np.log(3e3), n))
+    sig[:500] = 1e6
+    mu = rng.uniform(-1, 1, n) * np.maximum(sig, 1) * rng.choice([1, 10, 1000], n)
+    u = rng.random(n)
+    u[:50] = 0.0
+    u[50:100] = 1.0 - 2.0 ** -53
+    z_em, ln_em = ctx.sample_z(mu, sig, u)
+    z_tb, ln_tb = ctx.sample_z(mu, sig, u, table=True)
+    assert np.array_equal(z_em, z_tb)
+    np.testing.assert_allclose(ln_em, ln_tb, rtol=1e-13, atol=1e-13)
+    idx = rng.choice(n, 3000, replace=False)
+    z_or = np.array([oracle.sample_z(mu[i], sig[i], u[i])[0] for i in idx])
+    assert np.array_equal(z_em[idx], z_or)
