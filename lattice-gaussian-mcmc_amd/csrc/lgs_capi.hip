@@ -70,6 +70,14 @@ struct Timer {
     hipEvent_t a, b;
 };
 
+struct BzCall {  // an int8-digit B z launch, replayed in fp64 if a digit overflowed
+    const void* Z;
+    bool z64;
+    int64_t ldz, n;
+    double* V;
+    int64_t rb, rstride, roff;
+};
+
 }  // namespace
 
 struct lgs_ctx {
@@ -81,9 +89,13 @@ struct lgs_ctx {
     double sigma = 0;
     int precision = 10;
     uint32_t basis_flags = 0;
-    int panel = 32;
+    int panel = 16;
     bool has_B = false;
     DevBuf R, RP, RC, BT, coord;  // coord: cp | rii | sig | sig_ref | lterm (5 x d)
+    DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
+    bool has_Bi8 = false;
+    int64_t bd_rows = 0, bd_cols = 0;
+    std::vector<BzCall> pending_i8;
     // scratch
     DevBuf Z, LW, V, sel, fsel, cnt, ccnt, flags, stage_a, stage_b, stage_c, stage_d, stage_e,
         stage_f, stage_g, vs;
@@ -135,8 +147,34 @@ struct Scope {  // times one launch when timing is enabled
     }
 };
 
-int finish(lgs_ctx* c) {  // sync, fold timers, report kernel flags
+int run_bz_fp64(lgs_ctx* c, const BzCall& b);
+
+// Wait for the stream; if an int8-digit B z saw a coefficient beyond two digits,
+// replay the pending B z launches with the fp64 kernel.  Must run before any
+// copy that consumes their output.
+int settle_bz(lgs_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->pending_i8.empty()) return LGS_OK;
+    {
+        unsigned int f0 = 0;
+        HIP_TRY(hipMemcpy(&f0, c->flags.p, sizeof(f0), hipMemcpyDeviceToHost));
+        if (f0 & lgs::kFlagI8Range) {  // coefficients beyond two int8 digits: redo in fp64
+            for (const auto& b : c->pending_i8) {
+                int rc = run_bz_fp64(c, b);
+                if (rc) return rc;
+            }
+            const unsigned int keep = f0 & ~lgs::kFlagI8Range;
+            HIP_TRY(hipMemcpyAsync(c->flags.p, &keep, sizeof(keep), hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+        }
+        c->pending_i8.clear();
+    }
+    return LGS_OK;
+}
+
+int finish(lgs_ctx* c) {  // sync, fold timers, report kernel flags
+    int rc0 = settle_bz(c);
+    if (rc0) return rc0;
     for (auto& t : c->pending) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
@@ -188,10 +226,27 @@ int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, bool z64, void
     return LGS_OK;
 }
 
-int run_bz(lgs_ctx* c, const void* Z, bool z64, int64_t ldz, int64_t n, double* V) {
-    if (!c->has_B) return fail(LGS_ERR_STATE, "lattice points need B (lgs_set_basis B != NULL)");
+int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
     Scope s(c, 1);
-    HIP_TRY(lgs::launch::bz(Z, z64, ldz, c->BT.as<double>(), (int)c->d, n, V, c->d, c->stream));
+    HIP_TRY(lgs::launch::bz(b.Z, b.z64, b.ldz, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
+                            b.rstride, b.roff, c->stream));
+    return LGS_OK;
+}
+
+// v = B z: exact int8-digit MFMA kernel for integer bases (fp64 replay on digit
+// overflow, see finish()), fp64 MFMA kernel otherwise.  LGS_BZ_FP64=1 forces fp64.
+int run_bz(lgs_ctx* c, const void* Z, bool z64, int64_t ldz, int64_t n, double* V,
+           int64_t rb = 0, int64_t rstride = 0, int64_t roff = 0) {
+    if (!c->has_B) return fail(LGS_ERR_STATE, "lattice points need B (lgs_set_basis B != NULL)");
+    BzCall b{Z, z64, ldz, n, V, rb > 0 ? rb : n, rstride, roff};
+    static const bool force64 = getenv("LGS_BZ_FP64") && atoi(getenv("LGS_BZ_FP64")) == 1;
+    if (!c->has_Bi8 || force64) return run_bz_fp64(c, b);
+    Scope s(c, 1);
+    const int8_t* hi = c->Bd.as<int8_t>();
+    const int8_t* lo = hi + (size_t)c->bd_rows * c->bd_cols;
+    HIP_TRY(lgs::launch::bz_i8(Z, z64, ldz, hi, lo, (int)c->bd_cols, (int)c->d, n, V, c->d, b.rb,
+                               b.rstride, b.roff, c->flags.as<unsigned int>(), c->stream));
+    c->pending_i8.push_back(b);
     return LGS_OK;
 }
 
@@ -225,7 +280,7 @@ int lgs_create(lgs_ctx** out, int device) {
         return fail(LGS_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
     c->stream = c->own;
-    if (const char* p = getenv("LGS_PANEL")) c->panel = atoi(p) == 16 ? 16 : 32;
+    if (const char* p = getenv("LGS_PANEL")) c->panel = atoi(p) == 32 ? 32 : 16;
     if (const char* m = getenv("LGS_MAX_PROPOSALS")) {
         long long v = atoll(m);
         if (v >= 64) c->max_props = v;
@@ -320,6 +375,30 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
             for (size_t k = 0; k < dd; ++k) bt[k * dd + r] = B[r * dd + k];
         if ((rc = c->BT.reserve(dd * dd * 8))) return rc;
         HIP_TRY(hipMemcpy(c->BT.p, bt.data(), dd * dd * 8, hipMemcpyHostToDevice));
+        // exact int8-digit planes when B is integral with |B| <= 32639
+        bool ok = true;
+        for (size_t k = 0; k < dd * dd && ok; ++k)
+            ok = B[k] == std::nearbyint(B[k]) && std::fabs(B[k]) <= 32639.0;
+        c->has_Bi8 = ok;
+        if (ok) {
+            const int64_t rows = (d + 127) / 128 * 128, cols = (d + 63) / 64 * 64;
+            std::vector<int8_t> planes((size_t)2 * rows * cols, 0);
+            int8_t* hi = planes.data();
+            int8_t* lo = hi + (size_t)rows * cols;
+            for (size_t r = 0; r < dd; ++r)
+                for (size_t k = 0; k < dd; ++k) {
+                    const int v = (int)B[r * dd + k];
+                    const int l = (v << 24) >> 24;
+                    hi[r * cols + k] = (int8_t)((v - l) >> 8);
+                    lo[r * cols + k] = (int8_t)l;
+                }
+            if ((rc = c->Bd.reserve(planes.size()))) return rc;
+            HIP_TRY(hipMemcpy(c->Bd.p, planes.data(), planes.size(), hipMemcpyHostToDevice));
+            c->bd_rows = rows;
+            c->bd_cols = cols;
+        }
+    } else {
+        c->has_Bi8 = false;
     }
     c->d = d;
     c->sigma = sigma;
@@ -386,6 +465,7 @@ int lgs_klein(lgs_ctx* c, uint64_t seed, uint64_t first, int64_t n, void* z_out,
         if (v_out) {
             double* V = dev ? v_out + (size_t)off * d : c->V.as<double>();
             if ((rc = run_bz(c, Zp, z64, a.ldz, m, V))) return rc;
+            if ((rc = settle_bz(c))) return rc;
             if (!dev)
                 HIP_TRY(hipMemcpyAsync(v_out + (size_t)off * d, V, (size_t)m * d * 8,
                                        hipMemcpyDeviceToHost, c->stream));
@@ -393,7 +473,7 @@ int lgs_klein(lgs_ctx* c, uint64_t seed, uint64_t first, int64_t n, void* z_out,
         if (logw_out && !dev)
             HIP_TRY(hipMemcpyAsync(logw_out + off, a.LW, (size_t)m * 8, hipMemcpyDeviceToHost,
                                    c->stream));
-        if (!dev) {  // host staging buffers are reused by the next chunk
+        if (!dev || v_out) {  // staging buffers / the int8-digit replay need the chunk intact
             if ((rc = finish(c))) return rc;
         }
     }
@@ -431,6 +511,7 @@ int lgs_lattice_points(lgs_ctx* c, int64_t n, const void* z, double* v_out, uint
         V = c->V.as<double>();
     }
     if ((rc = run_bz(c, Zc, z64, n, n, V))) return rc;
+    if ((rc = settle_bz(c))) return rc;
     if (!dev) HIP_TRY(hipMemcpyAsync(v_out, V, (size_t)n * d * 8, hipMemcpyDeviceToHost, c->stream));
     return finish(c);
 }
@@ -510,8 +591,6 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         (rc = c->fsel.reserve((size_t)nc * 8)) || (rc = c->cnt.reserve((size_t)np * 4)) ||
         (rc = c->ccnt.reserve((size_t)nc * 4)))
         return rc;
-    if (v_samples && ((rc = c->V.reserve((size_t)np * d * 8)) || (rc = c->vs.reserve((size_t)nc * d * 8))))
-        return rc;
 
     // ---- device views of the chain state (staged through device buffers for host pointers)
     void* zs = z_state;
@@ -555,7 +634,7 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         a.counter_mode = 1;
         a.chain0 = (uint32_t)first_chain;
         a.step0 = 0;
-        a.nc = nc;
+        a.nt = 1;
         a.n = nc;
         a.ldz = nc;
         a.LW = c->LW.as<double>();
@@ -588,20 +667,11 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         a.counter_mode = 1;
         a.chain0 = (uint32_t)first_chain;
         a.step0 = (uint32_t)(first_step + (uint64_t)t0);
-        a.nc = nc;
+        a.nt = Tb;
         a.n = npb;
         a.ldz = npb;
         a.LW = c->LW.as<double>();
         if ((rc = run_klein(c, a, exact, wl, z64, c->Z.p))) return rc;
-        if (v_samples && kb > 0) {  // lattice points of the carried states, before they move
-            const void* zcm = zs;
-            if (!cm) {
-                if ((rc = c->stage_f.reserve((size_t)nc * d * zb))) return rc;
-                HIP_TRY(lgs::launch::to_coord_major(zs, z64, nc, (int)d, c->stage_f.p, z64, nc, c->stream));
-                zcm = c->stage_f.p;
-            }
-            if ((rc = run_bz(c, zcm, z64, nc, nc, c->vs.as<double>()))) return rc;
-        }
         if (moments) HIP_TRY(hipMemsetAsync(c->cnt.p, 0, (size_t)npb * 4, c->stream));
         lgs::AcceptArgs aa{};
         aa.nc = nc;
@@ -627,40 +697,25 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
             HIP_TRY(lgs::launch::moments(c->Z.p, z64, npb, c->cnt.as<int32_t>(), npb, (int)d, mom, c->stream));
             HIP_TRY(lgs::launch::moments_carry(zs, z64, cm, nc, (int)d, c->ccnt.as<int32_t>(), mom, c->stream));
         }
-        if (z_samples && kb > 0) {
-            // kept states -> rows (chain, first_keep + k) of the n_chains x n_keep x d output
+        if ((z_samples || v_samples) && kb > 0) {
+            // kept states q = chain*kb + k, gathered coordinate-major (d x nq); chain-major
+            // proposal order makes this a near-contiguous copy
             const int64_t nq = nc * kb;
-            void* out;
-            if (dev && !cm && kb == n_keep) {
-                out = z_samples;
-            } else {
-                if ((rc = c->stage_f.reserve((size_t)nq * d * zb))) return rc;
-                out = c->stage_f.p;
-            }
+            if ((rc = c->stage_f.reserve((size_t)nq * d * zb))) return rc;
             HIP_TRY(lgs::launch::gather_z(c->Z.p, z64, npb, c->sel.as<int64_t>(), nq, kb, zs, cm, nc,
-                                          (int)d, out, 0, c->stream));
-            if (out != z_samples) {
+                                          (int)d, c->stage_f.p, 1, c->stream));
+            if (v_samples) {  // rows (chain, first_keep + k) of the n_chains x n_keep x d output
+                if ((rc = run_bz(c, c->stage_f.p, z64, nq, nq, v_samples, kb, n_keep, first_keep)))
+                    return rc;
+            }
+            if (z_samples) {
+                if ((rc = c->stage_g.reserve((size_t)nq * d * zb))) return rc;
+                HIP_TRY(lgs::launch::transpose_out(c->stage_f.p, z64, nq, nq, (int)d, c->stage_g.p,
+                                                   z64, c->stream));
                 HIP_TRY(hipMemcpy2DAsync((char*)z_samples + (size_t)first_keep * d * zb,
-                                         (size_t)n_keep * d * zb, out, (size_t)kb * d * zb,
+                                         (size_t)n_keep * d * zb, c->stage_g.p, (size_t)kb * d * zb,
                                          (size_t)kb * d * zb, nc, kind_of(dev, true), c->stream));
             }
-        }
-        if (v_samples && kb > 0) {
-            const int64_t nq = nc * kb;
-            if ((rc = run_bz(c, c->Z.p, z64, npb, npb, c->V.as<double>()))) return rc;
-            double* out;
-            if (kb == n_keep) {
-                out = v_samples;
-            } else {
-                if ((rc = c->stage_g.reserve((size_t)nq * d * 8))) return rc;
-                out = c->stage_g.as<double>();
-            }
-            HIP_TRY(lgs::launch::gather_v(c->V.as<double>(), c->sel.as<int64_t>(), nq, kb,
-                                          c->vs.as<double>(), (int)d, out, c->stream));
-            if (out != v_samples)
-                HIP_TRY(hipMemcpy2DAsync(v_samples + (size_t)first_keep * d, (size_t)n_keep * d * 8, out,
-                                         (size_t)kb * d * 8, (size_t)kb * d * 8, nc,
-                                         hipMemcpyDeviceToDevice, c->stream));
         }
         // chain states after the block (in place; carried chains keep their row)
         HIP_TRY(lgs::launch::gather_z(c->Z.p, z64, npb, c->fsel.as<int64_t>(), nc, 1, zs, cm, nc,

@@ -186,8 +186,16 @@ __device__ __forceinline__ double em_P(double x, double mu, double sig, double i
     return fma(-em_H(t, is), fx, sig * kSqrtHalfPi * erf(t * kInvSqrt2));
 }
 
-__device__ __forceinline__ SampleZOut sample_z(double mu, double sig, int precision,
-                                               bool linear_probs, double u) {
+// Not inlined: inlining lets the compiler hoist the ~100 polynomial constants of
+// erf/erfinv/exp/log out of the coordinate loop into registers (measured: 398
+// VGPR+AGPR, 1 wave/SIMD); as a call the kernel stays at <= 170 VGPRs.
+#ifndef LGS_SAMPLEZ_INLINE
+#define LGS_SAMPLEZ_ATTR __device__ __noinline__
+#else
+#define LGS_SAMPLEZ_ATTR __device__ __forceinline__
+#endif
+LGS_SAMPLEZ_ATTR SampleZOut sample_z(double mu, double sig, int precision, bool linear_probs,
+                                     double u) {
     if (sig < kEMMin) return sample_z_table(mu, sig, precision, linear_probs, u);
     int64_t lo, hi;
     support_window(mu, sig, precision, lo, hi);

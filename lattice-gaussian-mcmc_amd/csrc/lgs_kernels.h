@@ -8,6 +8,7 @@ namespace lgs {
 
 constexpr unsigned int kFlagNonFinite = 1u;  // a conditional mean was NaN/inf
 constexpr unsigned int kFlagOverflow = 2u;   // |z| >= 2^31 with an int32 store
+constexpr unsigned int kFlagI8Range = 4u;    // |z| > 32639: int8-digit B z must be redone in fp64
 
 // Per-launch arguments of the Klein samplers.  Per-coordinate arrays (length d):
 //   cp      c' = Q^T c
@@ -20,7 +21,7 @@ struct KleinArgs {
     int d;
     int precision;
     int linear_probs;
-    int counter_mode;  // 0: lane p -> sample base+p; 1: chain0 + p%nc, step0 + p/nc
+    int counter_mode;  // 0: lane p -> sample base+p; 1: chain0 + p/nt, step0 + p%nt (chain-major)
     const double* cp;
     const double* rii;
     const double* sig;
@@ -31,7 +32,7 @@ struct KleinArgs {
     uint64_t base;
     uint32_t chain0;
     uint32_t step0;
-    int64_t nc;
+    int64_t nt;
     int64_t n;
     int64_t ldz;
     double* LW;
@@ -77,7 +78,11 @@ hipError_t transpose_out(const void* Z, bool z64, int64_t ldz, int64_t n, int d,
                          bool out64, hipStream_t st);
 hipError_t to_coord_major(const void* in, bool in64, int64_t n, int d, void* Z, bool z64,
                           int64_t ldz, hipStream_t st);
+// V row of sample s: (s / rb) * rstride + roff + s % rb (rb = n, rstride = roff = 0: row s)
 hipError_t bz(const void* Z, bool z64, int64_t ldz, const double* BT, int d, int64_t n, double* V,
-              int64_t ldv, hipStream_t st);
+              int64_t ldv, int64_t rb, int64_t rstride, int64_t roff, hipStream_t st);
+hipError_t bz_i8(const void* Z, bool z64, int64_t ldz, const int8_t* Bd1, const int8_t* Bd0, int dc,
+                 int d, int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
+                 unsigned int* flags, hipStream_t st);
 }  // namespace launch
 }  // namespace lgs

@@ -31,8 +31,8 @@ __device__ __forceinline__ void lane_counter(const KleinArgs& a, int64_t p, uint
         chain = (uint32_t)s;
         step = (uint32_t)(s >> 32);
     } else {
-        chain = a.chain0 + (uint32_t)(p % a.nc);
-        step = a.step0 + (uint32_t)(p / a.nc);
+        chain = a.chain0 + (uint32_t)(p / a.nt);
+        step = a.step0 + (uint32_t)(p % a.nt);
     }
 }
 
@@ -208,7 +208,8 @@ __global__ __launch_bounds__(256) void samplez_probe_kernel(const double* __rest
 }
 
 // ------------------------------------------------------------ IMHK accept
-// One lane per chain; proposals of step t for chain c live at p = t*nc + c.
+// One lane per chain; proposals of step t for chain c live at p = c*T + t
+// (chain-major, so the kept states of a chain are contiguous columns).
 // sel[c*n_keep + k] = proposal index of the state retained after step
 // (k+1)*thin (-1 = the carried-in state); cnt[p] / cnt_carry[c] count the
 // retained steps spent in each state (moments), final_sel[c] = last state.
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
     int32_t carry = 0;
     const uint32_t chain = a.chain0 + (uint32_t)c;
     for (int64_t t = 0; t < a.T; ++t) {
-        const int64_t p = t * a.nc + c;
+        const int64_t p = c * a.T + t;
         const double lw_y = a.LW[p];
         double ratio;
         if (lw_x == -INFINITY) {
@@ -417,7 +418,8 @@ template <typename ZT>
 __global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, int64_t ldz,
                                                       const double* __restrict__ BT, int d,
                                                       int64_t n, double* __restrict__ V,
-                                                      int64_t ldv) {
+                                                      int64_t ldv, int64_t rb, int64_t rstride,
+                                                      int64_t roff) {
     constexpr int BM = 64, BN = 64, KC = 16, LDP = 80;  // LDP: padded row (doubles)
     __shared__ double As[KC][LDP];
     __shared__ double Bs[KC][LDP];
@@ -468,8 +470,128 @@ __global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, 
             for (int reg = 0; reg < 4; ++reg) {
                 const int64_t s = s0 + wm * 32 + a * 16 + (lane >> 4) + 4 * reg;
                 const int r = r0 + wn * 32 + b * 16 + (lane & 15);
-                if (s < n && r < d) V[(size_t)s * ldv + r] = acc[a][b][reg];
+                if (s < n && r < d) {
+                    const int64_t row = (s / rb) * rstride + roff + s % rb;
+                    V[(size_t)row * ldv + r] = acc[a][b][reg];
+                }
             }
+}
+
+// ------------------------------------------------------------ B z, exact int8 MFMA
+// For integer bases with |B| <= 32639 and coefficients |z| <= 32639 the lattice
+// points are computed exactly with two balanced base-256 digits per operand
+// (x = 256 x1 + x0, x0, x1 in [-128, 127]) on v_mfma_i32_32x32x32_i8:
+//   v = 65536 * (B1 z1) + 256 * (B1 z0 + B0 z1) + B0 z0,
+// three int32 accumulators (|partial| <= 2 d 2^14 < 2^31 for d <= 65536),
+// combined in int64 and converted to fp64 (exact below 2^53).  A coefficient out
+// of range sets kFlagI8Range and the host recomputes with the fp64 kernel.
+// Block tile 64 samples x 128 coords, K chunks of 64 through LDS; waves 2x2, each
+// 32 samples x 64 coords = two 32x32 MFMA tiles.  Operand maps (32x32x32 i8):
+// A row / B column = lane & 31, 16 consecutive k per lane (k = 16*(lane>>5) + j;
+// any k permutation shared by A and B gives the same sum); D: col = lane & 31,
+// row = (reg & 3) + 8*(reg >> 2) + 4*(lane >> 5).
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v16i_t __attribute__((ext_vector_type(16)));
+
+template <typename ZT>
+__global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z, int64_t ldz,
+                                                    const int8_t* __restrict__ Bd1,
+                                                    const int8_t* __restrict__ Bd0, int dc, int d,
+                                                    int64_t n, double* __restrict__ V, int64_t ldv,
+                                                    int64_t rb, int64_t rstride, int64_t roff,
+                                                    unsigned int* flags) {
+    constexpr int BM = 64, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
+    __shared__ __attribute__((aligned(16))) int8_t Zs1[BM * P], Zs0[BM * P], Bs1[BN * P], Bs0[BN * P];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int r0 = blockIdx.x * BN;
+    const int64_t s0 = (int64_t)blockIdx.y * BM;
+    v16i_t p1[2], p2[2], p3[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        p1[t] = (v16i_t){};
+        p2[t] = (v16i_t){};
+        p3[t] = (v16i_t){};
+    }
+    bool bad = false;
+    const int zm = tid & 63, zq = tid >> 6;
+    for (int c0 = 0; c0 < d; c0 += KC) {
+        {  // z chunk -> balanced base-256 digits, [sample][k] byte planes
+            const int64_t s = s0 + zm;
+            const bool sok = s < n;
+            const ZT* zp = Z + (size_t)(c0 + zq * 16) * ldz + (sok ? s : 0);
+            v4i_t w0, w1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                unsigned int lo4 = 0, hi4 = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int c = c0 + zq * 16 + q * 4 + j;
+                    const ZT zr = (sok && c < d) ? zp[(size_t)(q * 4 + j) * ldz] : (ZT)0;
+                    bad |= (zr > (ZT)32639) | (zr < (ZT)-32639);
+                    const int z = (int)zr;
+                    const int lo = (z << 24) >> 24;  // balanced low digit in [-128, 127]
+                    const int hi = (z - lo) >> 8;
+                    lo4 |= ((unsigned int)lo & 0xffu) << (8 * j);
+                    hi4 |= ((unsigned int)hi & 0xffu) << (8 * j);
+                }
+                w0[q] = (int)lo4;
+                w1[q] = (int)hi4;
+            }
+            *(v4i_t*)&Zs0[zm * P + zq * 16] = w0;
+            *(v4i_t*)&Zs1[zm * P + zq * 16] = w1;
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {  // B digit planes [coord][k], 16 B per thread per plane
+            const int idx = tid + 256 * e;
+            const int row = idx >> 2, part = idx & 3;
+            const size_t g = (size_t)(r0 + row) * dc + c0 + part * 16;
+            *(v4i_t*)&Bs1[row * P + part * 16] = *(const v4i_t*)&Bd1[g];
+            *(v4i_t*)&Bs0[row * P + part * 16] = *(const v4i_t*)&Bd0[g];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int kb = ks * 32 + 16 * (lane >> 5);
+            const int arow = wm * 32 + (lane & 31);
+            const v4i_t a1 = *(const v4i_t*)&Zs1[arow * P + kb];
+            const v4i_t a0 = *(const v4i_t*)&Zs0[arow * P + kb];
+#pragma unroll
+            for (int tn = 0; tn < 2; ++tn) {
+                const int col = wn * 64 + tn * 32 + (lane & 31);
+                const v4i_t b1 = *(const v4i_t*)&Bs1[col * P + kb];
+                const v4i_t b0 = *(const v4i_t*)&Bs0[col * P + kb];
+                p1[tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, p1[tn], 0, 0, 0);
+                p2[tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, p2[tn], 0, 0, 0);
+                p2[tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, p2[tn], 0, 0, 0);
+                p3[tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, p3[tn], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    // output rows: sample q -> (q / rb) * rstride + roff + q % rb, in 32-bit pieces
+    const int64_t qb = s0 + wm * 32;
+    const int64_t cb = qb / rb;
+    const unsigned int kb0 = (unsigned int)(qb - cb * rb), urb = (unsigned int)rb;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+        const int64_t s = qb + row;
+        if (s >= n) continue;
+        const unsigned int kk = kb0 + (unsigned int)row;
+        const unsigned int wrap = kk / urb;
+        const int64_t orow = (cb + wrap) * rstride + roff + (kk - wrap * urb);
+        double* vrow = V + (size_t)orow * ldv;
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+            const int r = r0 + wn * 64 + tn * 32 + (lane & 31);
+            if (r < d) {
+                const long long v = 65536LL * p1[tn][reg] + 256LL * p2[tn][reg] + (long long)p3[tn][reg];
+                vrow[r] = (double)v;
+            }
+        }
+    }
+    if (bad) atomicOr(flags, kFlagI8Range);
 }
 
 // ============================================================ launchers
@@ -604,13 +726,25 @@ hipError_t to_coord_major(const void* in, bool in64, int64_t n, int d, void* Z, 
 }
 
 hipError_t bz(const void* Z, bool z64, int64_t ldz, const double* BT, int d, int64_t n, double* V,
-              int64_t ldv, hipStream_t st) {
+              int64_t ldv, int64_t rb, int64_t rstride, int64_t roff, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
     if (z64)
-        hipLaunchKernelGGL(bz_gemm_kernel<int64_t>, grid, dim3(256), 0, st, (const int64_t*)Z, ldz, BT, d, n, V, ldv);
+        hipLaunchKernelGGL(bz_gemm_kernel<int64_t>, grid, dim3(256), 0, st, (const int64_t*)Z, ldz, BT, d, n, V, ldv, rb, rstride, roff);
     else
-        hipLaunchKernelGGL(bz_gemm_kernel<int32_t>, grid, dim3(256), 0, st, (const int32_t*)Z, ldz, BT, d, n, V, ldv);
+        hipLaunchKernelGGL(bz_gemm_kernel<int32_t>, grid, dim3(256), 0, st, (const int32_t*)Z, ldz, BT, d, n, V, ldv, rb, rstride, roff);
+    return hipGetLastError();
+}
+
+hipError_t bz_i8(const void* Z, bool z64, int64_t ldz, const int8_t* Bd1, const int8_t* Bd0, int dc,
+                 int d, int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
+                 unsigned int* flags, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((d + 127) / 128), (unsigned)((n + 63) / 64));
+    if (z64)
+        hipLaunchKernelGGL(bz_i8_kernel<int64_t>, grid, dim3(256), 0, st, (const int64_t*)Z, ldz, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags);
+    else
+        hipLaunchKernelGGL(bz_i8_kernel<int32_t>, grid, dim3(256), 0, st, (const int32_t*)Z, ldz, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags);
     return hipGetLastError();
 }
 

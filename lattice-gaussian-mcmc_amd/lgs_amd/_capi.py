@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "liblgs_hip.so")
+LIB_PATH = os.environ.get("LGS_LIB") or os.path.join(_HERE, "_lib", "liblgs_hip.so")
 
 LGS_OK = 0
 LGS_ERR_INVALID = -1

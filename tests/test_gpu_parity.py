@@ -296,3 +296,48 @@ def test_samplez_em_vs_table_vs_oracle_stress(ctx, oracle):
     idx = rng.choice(n, 3000, replace=False)
     z_or = np.array([oracle.sample_z(mu[i], sig[i], u[i])[0] for i in idx])
     assert np.array_equal(z_em[idx], z_or)
+
+
+# ------------------------------------------------------------------ B z kernels
+@pytest.mark.parametrize("zmax", [1500, 32639, 40000, 10 ** 7])
+def test_lattice_points_integer_basis_exact(ctx, zmax):
+    """Int8-digit MFMA path (|z| <= 32639) and its fp64 replay (larger |z|) are exact."""
+    from lgs_amd.lattices import ntru_basis
+    B = ntru_basis(64, 12289, 3)
+    R, cp = np.linalg.qr(B)[1], np.zeros(128)
+    R = R * np.where(np.diag(R) < 0, -1.0, 1.0)[:, None]
+    ctx.set_basis(R, cp, B, 165.7)
+    rng = np.random.default_rng(zmax)
+    z = rng.integers(-zmax, zmax + 1, size=(777, 128)).astype(np.int64)
+    z[0, :] = zmax
+    z[1, :] = -zmax
+    v = ctx.lattice_points(z)
+    assert np.array_equal(v, (B @ z.T).T)
+
+
+def test_imhk_device_v_samples(ctx, capi):
+    import torch
+    g = load_golden("klein_qary128.npz")
+    R, cp, B = golden_R(g)
+    ctx.set_basis(R, cp, B, float(g["sigma"]))
+    d, nc, steps, thin = R.shape[0], 64, 12, 2
+    dev = "cuda:0"
+    z = torch.zeros((d, nc), dtype=torch.int32, device=dev)
+    lw = torch.zeros(nc, dtype=torch.float64, device=dev)
+    init = torch.zeros(nc, dtype=torch.int32, device=dev)
+    acc = torch.zeros(nc, dtype=torch.int64, device=dev)
+    zs = torch.zeros((nc, steps // thin, d), dtype=torch.int32, device=dev)
+    vs = torch.zeros((nc, steps // thin, d), dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    f = capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR
+    # z_samples is row-major only; pass a row-major z_state for that call
+    ctx.imhk(9, 0, nc, 1, steps, thin, z, lw, init, acc, v_samples=vs, flags=f)
+    zr = torch.zeros((nc, d), dtype=torch.int32, device=dev)
+    lw2 = torch.zeros(nc, dtype=torch.float64, device=dev)
+    init2 = torch.zeros(nc, dtype=torch.int32, device=dev)
+    acc2 = torch.zeros(nc, dtype=torch.int64, device=dev)
+    ctx.imhk(9, 0, nc, 1, steps, thin, zr, lw2, init2, acc2, z_samples=zs, flags=capi.LGS_DEVICE_PTRS)
+    zsn = zs.cpu().numpy().astype(np.int64)
+    assert np.array_equal(vs.cpu().numpy(), np.einsum("rc,nkc->nkr", B, zsn))
+    assert np.array_equal(z.cpu().numpy().T, zr.cpu().numpy())
+    assert torch.equal(acc, acc2)

@@ -1,0 +1,56 @@
+"""Klein-kernel micro-benchmark: device time of lgs_klein at a BASELINE config.
+
+usage: python tools/kbench.py [--config C3_ntru512] [--n 262144] [--reps 3] [--exact]
+Prints one JSON line per library in $LGS_LIBS (colon-separated .so paths) or the
+default library."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "lattice-gaussian-mcmc_amd"))
+
+
+def run_one(args):
+    import numpy as np
+    import torch
+    from lgs_amd import _capi
+    from lgs_amd.lattices import build_config
+    lat, sigma = build_config(args.config)
+    B = lat.basis
+    d = B.shape[0]
+    Q, R = np.linalg.qr(B)
+    R = np.ascontiguousarray(R * np.where(np.diag(R) < 0, -1.0, 1.0)[:, None])
+    ctx = _capi.Context(0)
+    ctx.set_basis(R, np.zeros(d), B, sigma)
+    n = args.n
+    z = torch.empty((d, n), dtype=torch.int32, device="cuda:0")
+    lw = torch.empty(n, dtype=torch.float64, device="cuda:0")
+    flags = _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR | (_capi.LGS_EXACT_ORDER if args.exact else 0)
+    ctx.klein(1, 0, n, z, None, lw, flags)
+    ctx.timing_enable(True)
+    for r in range(args.reps):
+        ctx.klein(1, (r + 1) * n, n, z, None, lw, flags)
+    ms, k = ctx.timing_get(_capi.KERNEL_KLEIN)
+    avg = ms / k
+    print(json.dumps({"lib": os.environ.get("LGS_LIB", "default"), "config": args.config, "d": d, "n": n,
+                      "kernel_ms": round(avg, 3), "samples_per_s": round(n / avg * 1e3, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3_ntru512")
+    ap.add_argument("--n", type=int, default=1 << 18)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--exact", action="store_true")
+    ap.add_argument("--one", action="store_true")
+    args = ap.parse_args()
+    libs = os.environ.get("LGS_LIBS")
+    if args.one or not libs:
+        run_one(args)
+    else:
+        for lib in libs.split(":"):
+            env = dict(os.environ, LGS_LIB=lib)
+            subprocess.run([sys.executable, __file__, "--one"] + sys.argv[1:], env=env, check=True, timeout=600)
