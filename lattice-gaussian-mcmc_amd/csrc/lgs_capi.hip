@@ -91,7 +91,7 @@ struct lgs_ctx {
     uint32_t basis_flags = 0;
     int panel = 16;
     bool has_B = false;
-    DevBuf R, RP, RC, BT, coord;  // coord: cp | rii | sig | sig_ref | lterm (5 x d)
+    DevBuf R, RP, RC, BT, coord;  // coord: cp | rii | sig | sig_ref | lterm | irii | ros | isr
     DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
     bool has_Bi8 = false;
     int64_t bd_rows = 0, bd_cols = 0;
@@ -213,16 +213,27 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
     a.sig = co + 2 * d;
     a.sig_ref = co + 3 * d;
     a.lterm = co + 4 * d;
+    a.irii = co + 5 * d;
+    a.ros = co + 6 * d;
+    a.isr = co + 7 * d;
     a.sigma = c->sigma;
     a.seed = seed;
     a.flags = c->flags.as<unsigned int>();
     return a;
 }
 
+// Kernel choice: exact order on request; otherwise the MFMA far-field kernel when
+// the launch is whole waves with 16-B aligned coefficient rows (panel 16), else
+// the VALU panel kernel.  LGS_KERNEL=valu forces the VALU kernel.
 int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, bool z64, void* Z) {
     Scope s(c, 0);
-    HIP_TRY(lgs::launch::klein(a, c->R.as<double>(), c->RP.as<double>(), c->RC.as<double>(),
-                               c->panel, exact, wl, z64, Z, c->stream));
+    static const bool force_valu = getenv("LGS_KERNEL") && strcmp(getenv("LGS_KERNEL"), "valu") == 0;
+    int panel = c->panel;
+    if (!exact && !force_valu && c->panel == 16 && a.n % 64 == 0 && a.ldz % 4 == 0 &&
+        ((uintptr_t)Z % 16) == 0)
+        panel = 0;
+    HIP_TRY(lgs::launch::klein(a, c->R.as<double>(), c->RP.as<double>(), c->RC.as<double>(), panel,
+                               exact, wl, z64, Z, c->stream));
     return LGS_OK;
 }
 
@@ -322,7 +333,7 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     const int PB = c->panel;
     const size_t dd = (size_t)d;
     // per-coordinate parameters (klein.py:195-211, 255-263)
-    std::vector<double> co(5 * dd);
+    std::vector<double> co(8 * dd);
     for (size_t i = 0; i < dd; ++i) {
         const double rii = R[i * dd + i];
         if (rii == 0.0 || !std::isfinite(rii))
@@ -338,6 +349,9 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
         co[2 * dd + i] = s;
         co[3 * dd + i] = sref;
         co[4 * dd + i] = 0.5 * std::log(2.0 * M_PI) + std::log(sref);
+        co[5 * dd + i] = 1.0 / rii;
+        co[6 * dd + i] = rii / sigma;
+        co[7 * dd + i] = 1.0 / sref;
     }
     // panel layouts (lgs_kernels.hip, klein_panel_kernel)
     const int64_t npan = (d + PB - 1) / PB;

@@ -101,8 +101,9 @@ struct SampleZOut {
 // scipy's logsumexp: the normalisation cancels in cdf = cumsum / cumsum[-1], so
 // the decision is the reference's up to ulp-level rounding of the boundaries.
 // Two passes over the window (sum, then cumulative walk); no table storage.
-__device__ __forceinline__ SampleZOut sample_z_table(double mu, double sig, int precision,
-                                                     bool linear_probs, double u) {
+__device__ __noinline__ SampleZOut sample_z_table(double mu, double sig, int precision,
+                                                  bool linear_probs, double u,
+                                                  bool want_log = true) {
     int64_t lo, hi;
     support_window(mu, sig, precision, lo, hi);
     int64_t ks = (int64_t)rint(mu);
@@ -136,7 +137,7 @@ __device__ __forceinline__ SampleZOut sample_z_table(double mu, double sig, int 
         }
     }
     out.z = z;
-    out.log_norm = shift + log(S);
+    out.log_norm = want_log ? shift + log(S) : 0.0;
     return out;
 }
 
@@ -180,7 +181,7 @@ __device__ __forceinline__ double em_H(double t, double is) {
     return res;
 }
 
-__device__ __forceinline__ double em_P(double x, double mu, double sig, double is, double& fx) {
+__device__ __noinline__ double em_P(double x, double mu, double sig, double is, double& fx) {
     const double t = (x - mu) * is;
     fx = exp(-0.5 * (t * t));
     return fma(-em_H(t, is), fx, sig * kSqrtHalfPi * erf(t * kInvSqrt2));
@@ -194,9 +195,64 @@ __device__ __forceinline__ double em_P(double x, double mu, double sig, double i
 #else
 #define LGS_SAMPLEZ_ATTR __device__ __forceinline__
 #endif
+// Windows of at most 4 points (sigma < 0.1 gives at most 3): exponents first,
+// max-shift, and exp() only for the terms that do not underflow relative to the
+// largest (e - e_max < -745.2 gives exactly 0.0 in fp64, as exp would), so the
+// common near-deterministic case costs one exponent per point and no exp.
+// Same decision rule as sample_z_table: smallest k with cumsum > u * sum.
+__device__ __forceinline__ bool sample_z_small(double mu, double sig, int precision,
+                                               bool linear_probs, double u, bool want_log,
+                                               SampleZOut& out) {
+    int64_t lo, hi;
+    support_window(mu, sig, precision, lo, hi);
+    if (hi - lo > 3) return false;
+    const int n = (int)(hi - lo) + 1;
+    const double is = 1.0 / sig;
+    double e[4];
+    double emax = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double t = (((double)lo + (double)k) - mu) * is;
+        e[k] = k < n ? -0.5 * (t * t) : -INFINITY;
+        emax = fmax(emax, e[k]);
+    }
+    if (linear_probs && emax < -745.2) {  // every probability underflows: round(mean)
+        out.z = (int64_t)rint(mu);
+        out.log_norm = -INFINITY;
+        return true;
+    }
+    double w[4];
+    double S = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double x = e[k] - emax;
+        w[k] = x == 0.0 ? 1.0 : (x < -745.2 ? 0.0 : exp(x));
+        S += w[k];
+    }
+    const double target = u * S;
+    double C = 0.0;
+    int64_t z = hi;
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        C += w[k];
+        if (!found && k < n && C > target) {
+            z = lo + k;
+            found = true;
+        }
+    }
+    out.z = z;
+    out.log_norm = want_log ? emax + log(S) : 0.0;
+    return true;
+}
+
 LGS_SAMPLEZ_ATTR SampleZOut sample_z(double mu, double sig, int precision, bool linear_probs,
-                                     double u) {
-    if (sig < kEMMin) return sample_z_table(mu, sig, precision, linear_probs, u);
+                                     double u, bool want_log = true) {
+    if (sig < kEMMin) {
+        SampleZOut o;
+        if (sample_z_small(mu, sig, precision, linear_probs, u, want_log, o)) return o;
+        return sample_z_table(mu, sig, precision, linear_probs, u, want_log);
+    }
     int64_t lo, hi;
     support_window(mu, sig, precision, lo, hi);
     const double is = 1.0 / sig;
@@ -227,12 +283,11 @@ LGS_SAMPLEZ_ATTR SampleZOut sample_z(double mu, double sig, int precision, bool 
     }
     const double margin = fmin(Ck - target, kd > flo ? target - (Ck - fk) : target);
     if (!(margin > 1e-12 * S) || !(Ck > target)) {
-        SampleZOut o = sample_z_table(mu, sig, precision, linear_probs, u);
-        return o;
+        return sample_z_table(mu, sig, precision, linear_probs, u, want_log);
     }
     SampleZOut out;
     out.z = (int64_t)kd;
-    out.log_norm = log(S);
+    out.log_norm = want_log ? log(S) : 0.0;
     return out;
 }
 

@@ -17,6 +17,8 @@ constexpr unsigned int kFlagI8Range = 4u;    // |z| > 32639: int8-digit B z must
 //           0 when sigma/R_ii < 1e-10 (deterministic rounding)
 //   sig_ref sigma/R_ii unclamped (reference-mode weight, klein.py:255-263)
 //   lterm   0.5*log(2*pi) + log(sig_ref)
+//   irii    1/R_ii, ros = R_ii/sigma, isr = 1/sig_ref (reciprocal forms for the
+//           fast kernels; the exact-order kernel divides like the reference)
 struct KleinArgs {
     int d;
     int precision;
@@ -27,6 +29,9 @@ struct KleinArgs {
     const double* sig;
     const double* sig_ref;
     const double* lterm;
+    const double* irii;
+    const double* ros;
+    const double* isr;
     double sigma;
     uint64_t seed;
     uint64_t base;

@@ -47,11 +47,16 @@ __device__ __forceinline__ int64_t decide_coord(const KleinArgs& a, int i, doubl
         flags |= kFlagNonFinite;
         return 0;
     }
+#ifdef LGS_DIAG_NO_SAMPLEZ
+    if (true) {  // diagnostic build: SampleZ replaced by rounding
+        zi = (int64_t)rint(mu + rs.u((uint32_t)(a.d - 1 - i)) * 1e-300);
+    } else
+#endif
     if (s == 0.0) {  // sigma_i < 1e-10: round, no draw (klein.py:201-204)
         zi = (int64_t)rint(mu);
     } else {
         SampleZOut o = sample_z(mu, s, a.precision, a.linear_probs != 0,
-                                rs.u((uint32_t)(a.d - 1 - i)));
+                                rs.u((uint32_t)(a.d - 1 - i)), WL);
         zi = o.z;
         if (WL) lw += o.log_norm;
     }
@@ -59,8 +64,8 @@ __device__ __forceinline__ int64_t decide_coord(const KleinArgs& a, int i, doubl
         // Reference-mode importance weight (imhk.py:102-124): log_gaussian_weight(Bz)
         // - compute_log_density(Bz), with ||Bz - c||^2 = sum_i (R_ii (z_i - mu_i))^2.
         const double res = (double)zi - mu;
-        const double ta = res * a.rii[i] / a.sigma;
-        const double tq = res / a.sig_ref[i];
+        const double ta = res * a.ros[i];
+        const double tq = res * a.isr[i];
         lw += (-0.5 * (ta * ta)) - (-0.5 * (tq * tq) - a.lterm[i]);
     }
     return zi;
@@ -146,7 +151,123 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
         }
         for (int s = 0; s < rows; ++s) {
             const int i = p_hi - 1 - s;
-            const double mu = (a.cp[i] - acc[PB - 1]) / a.rii[i];
+            const double mu = (a.cp[i] - acc[PB - 1]) * a.irii[i];
+            const int64_t zi = decide_coord<WL>(a, i, mu, rs, lw, flags);
+            store_z(Z, (size_t)i * ldz + p, zi, flags);
+            const double x = (double)zi;
+            const double* __restrict__ rc = RC + (size_t)i * (PB - 1);
+#pragma unroll
+            for (int k = 0; k < PB - 1; ++k) acc[k] = fma(rc[PB - 2 - k], x, acc[k]);
+#pragma unroll
+            for (int k = PB - 1; k >= 1; --k) acc[k] = acc[k - 1];
+            acc[0] = 0.0;
+        }
+    }
+    if (a.LW) a.LW[p] = lw;
+    if (flags) atomicOr(a.flags, flags);
+}
+
+// ------------------------------------------------------------ panel, MFMA far field
+// Same sampler and panel layout (PB = 16) as klein_panel_kernel, but the
+// far-field product of a panel -- F[16 rows][64 chains] = R_panel[16 x K] *
+// X[K x 64 chains], K = d - p_hi -- runs on the matrix cores of the wave:
+// v_mfma_f64_16x16x4_f64 with A = R tile (lane l: R[p_lo + (l&15)][j0 + (l>>4)],
+// one coalesced 512-B load) and B = coefficients (lane l loads 4 consecutive
+// chains of row j0 + (l>>4) as one 16-B load; MFMA g takes chain 4n+g, n = l&15).
+// D (lane l: rows (l>>4)+4*reg, chain 4*(l&15)+g) is transposed to one chain per
+// lane through a per-wave 8 KB LDS tile; the near field and SampleZ then run on
+// the VALU exactly as in klein_panel_kernel.  Requires n % 64 == 0, ldz % 4 == 0.
+// Coefficients written by other lanes are read back with L1-bypassing (nt) loads
+// after a wavefront release (s_waitcnt vmcnt(0)).
+typedef int v4i32_t __attribute__((ext_vector_type(4)));
+typedef double d4_t __attribute__((ext_vector_type(4)));
+
+template <typename ZT, bool WL>
+__global__ __launch_bounds__(256, 3) void klein_mfma_kernel(const KleinArgs a,
+                                                         const double* __restrict__ RP,
+                                                         const double* __restrict__ RC,
+                                                         ZT* __restrict__ Z) {
+    constexpr int PB = 16, LDF = 65;  // LDS tile pitch (doubles): conflict-free row reads
+    __shared__ double Fl[4][PB * LDF];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t p0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
+    if (p0 >= a.n) return;  // whole waves only (n % 64 == 0)
+    const int64_t p = p0 + lane;
+    uint32_t chain, step;
+    lane_counter(a, p, chain, step);
+    CoordStream rs;
+    rs.init(a.seed, step, chain);
+    const int d = a.d;
+    const size_t ldz = (size_t)a.ldz;
+    double lw = 0.0;
+    unsigned int flags = 0;
+    const int npan = (d + PB - 1) / PB;
+    double* F = Fl[wave];
+    const int kq = lane >> 4, nq = lane & 15;
+    double acc[PB];
+    for (int pk = 0; pk < npan; ++pk) {
+        const int p_hi = d - pk * PB;
+        const int rows = p_hi < PB ? p_hi : PB;
+#ifdef LGS_DIAG_NO_FAR
+        if (false) {
+#else
+        if (pk > 0) {
+#endif
+            // far field on the matrix cores; coefficients of rows >= p_hi were
+            // stored by this wave's lanes in earlier panels
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            d4_t f[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) f[g] = (d4_t){0.0, 0.0, 0.0, 0.0};
+            const double* __restrict__ rp = RP + (size_t)PB * PB * ((size_t)pk * (pk - 1) / 2);
+            const ZT* zcol = Z + p0 + 4 * nq;
+            // software pipeline, 4 stages: the loads of step j0+16 are issued while
+            // the MFMAs of step j0 run (VMEM returns in order, so each wait is a
+            // counted vmcnt); K = d - p_hi is a multiple of 16
+            double ra[4];
+            v4i32_t zb[4];
+            auto load_stage = [&](int jj, double& av, v4i32_t& zv) {
+                av = rp[(size_t)(jj - p_hi + kq) * PB + nq];
+                const ZT* zr = zcol + (size_t)(jj + kq) * ldz;
+                if (sizeof(ZT) == 4) {
+                    zv = __builtin_nontemporal_load((const v4i32_t*)zr);
+                } else {
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) zv[g] = (int)__builtin_nontemporal_load(zr + g);
+                }
+            };
+#pragma unroll
+            for (int st = 0; st < 4; ++st) load_stage(p_hi + 4 * st, ra[st], zb[st]);
+            for (int j0 = p_hi; j0 < d; j0 += 16) {
+#pragma unroll
+                for (int st = 0; st < 4; ++st) {
+                    const double a_cur = ra[st];
+                    const v4i32_t z_cur = zb[st];
+                    const int jn = j0 + 16 + 4 * st;
+                    if (jn < d) load_stage(jn, ra[st], zb[st]);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        f[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur, (double)z_cur[g], f[g], 0, 0, 0);
+                }
+            }
+            // D -> LDS [row][chain] -> one chain per lane
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) F[(kq + 4 * reg) * LDF + 4 * nq + g] = f[g][reg];
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < PB; ++r) acc[r] = F[r * LDF + lane];
+            __builtin_amdgcn_wave_barrier();
+        } else {
+#pragma unroll
+            for (int r = 0; r < PB; ++r) acc[r] = 0.0;
+        }
+        for (int s = 0; s < rows; ++s) {
+            const int i = p_hi - 1 - s;
+            const double mu = (a.cp[i] - acc[PB - 1]) * a.irii[i];
             const int64_t zi = decide_coord<WL>(a, i, mu, rs, lw, flags);
             store_z(Z, (size_t)i * ldz + p, zi, flags);
             const double x = (double)zi;
@@ -412,8 +533,6 @@ __global__ __launch_bounds__(256) void to_coord_major_kernel(const IT* __restric
 // D: row (l>>4)+4*reg, col l&15).  K staged through LDS in chunks of 16.
 // Exact (bit-identical to any summation order) when B and z are integers and
 // |partial sums| < 2^53.
-typedef double d4_t __attribute__((ext_vector_type(4)));
-
 template <typename ZT>
 __global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, int64_t ldz,
                                                       const double* __restrict__ BT, int d,
@@ -603,7 +722,12 @@ static hipError_t klein_t(const KleinArgs& a, const double* R, const double* RP,
     const dim3 block(256);
     const dim3 grid((unsigned)((a.n + 255) / 256));
     ZT* z = (ZT*)Z;
-    if (exact) {
+    if (!exact && panel == 0) {  // MFMA far field (panel rows fixed at 16)
+        if (wl)
+            hipLaunchKernelGGL((klein_mfma_kernel<ZT, true>), grid, block, 0, st, a, RP, RC, z);
+        else
+            hipLaunchKernelGGL((klein_mfma_kernel<ZT, false>), grid, block, 0, st, a, RP, RC, z);
+    } else if (exact) {
         if (wl)
             hipLaunchKernelGGL((klein_exact_kernel<ZT, true>), grid, block, 0, st, a, R, z);
         else
