@@ -52,36 +52,37 @@ def parse():
     ap.add_argument("--cpu-samples", type=int, default=1024, help="IMHK proposals for the CPU baseline")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic-csv", default=os.environ.get("LGS_TRAFFIC_CSV", ""),
+    ap.add_argument("--traffic-csv", default=os.environ.get(
+                        "LGS_TRAFFIC_CSV", os.path.join(REPO, "profiles", "r01_pmc_klein.csv")),
                     help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE")
     return ap.parse_args()
 
 
-def pmc_traffic(path, kernel_substr="klein_panel_kernel"):
-    """Per-launch HBM bytes of the Klein kernel from a rocprofv3 PMC CSV.
+def pmc_traffic(path, kernel_substr="klein_"):
+    """Per-launch HBM bytes of the Klein kernel from rocprofv3 --pmc CSVs.
 
-    FETCH_SIZE / WRITE_SIZE are in KB; on gfx950 FETCH_SIZE reports half of a
-    wide coalesced read (MI355X_MICROARCH.md §HBM), so it is doubled."""
+    `path` is a counter_collection.csv holding FETCH_SIZE and/or WRITE_SIZE rows
+    (tools/gpu_prof.sh collects them in separate passes and tools/summarize_prof.py
+    merges the Klein-kernel rows).  Only the largest dispatches (the bench's main
+    launches) are averaged.  FETCH_SIZE / WRITE_SIZE are in KB; on gfx950
+    FETCH_SIZE reports half of a wide coalesced read (MI355X_MICROARCH.md §HBM),
+    so it is doubled."""
     import csv
     if not path or not os.path.exists(path):
         return None
-    fetch, write, ids = {}, {}, set()
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            if kernel_substr not in row.get("Kernel_Name", ""):
-                continue
-            did = row.get("Dispatch_Id")
-            ids.add(did)
-            name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
-            if name == "FETCH_SIZE":
-                fetch[did] = val
-            elif name == "WRITE_SIZE":
-                write[did] = val
-    if not fetch:
+    rows = [r for r in csv.DictReader(open(path)) if kernel_substr in r.get("Kernel_Name", "")]
+    if not rows:
         return None
-    f_avg = 2.0 * 1024 * sum(fetch.values()) / len(fetch)
-    w_avg = 1024 * sum(write.values()) / len(write) if write else 0.0
-    return f_avg + w_avg
+    gmax = max(int(r["Grid_Size"]) for r in rows)
+    vals = {}
+    for r in rows:
+        if int(r["Grid_Size"]) == gmax:
+            vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    if "FETCH_SIZE" not in vals:
+        return None
+    fetch = 2.0 * 1024 * sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
+    write = 1024 * sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"]) if "WRITE_SIZE" in vals else 0.0
+    return fetch + write
 
 
 def main():
@@ -167,17 +168,25 @@ def main():
             dist.destroy_process_group()
         return
 
-    # ---- roofline of the dominant kernel (Klein sampler): per-launch algorithmic bytes / time
+    # ---- roofline of the dominant kernel (the Klein sampler), HIP-event timed on its
+    # launch stream.  It is FP64-compute bound: algorithmic work = d^2 flops per
+    # sample (the d^2/2 multiply-adds of klein.py:191-193), peak = FP64 dense
+    # (vector = matrix = 78.6 TF spec on MI355X).  The north_star's HBM view
+    # (B_alg bytes per sample) is reported beside it.
     units = nc * T
     k_avg_s = (k_ms / max(k_n, 1)) / 1e3
-    achieved = units * b_alg(d) / k_avg_s / 1e9
-    traffic = pmc_traffic(args.traffic_csv)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "klein_panel_kernel" if not args.exact_order else "klein_exact_kernel",
+    tflops = units * float(d) * d / k_avg_s / 1e12
+    traffic = pmc_traffic(args.traffic_csv, kernel_substr="klein_")
+    roofline = {"bound": "mfma", "achieved": round(tflops, 3), "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(tflops / FP64_PEAK_TFLOPS, 4),
+                "traffic": None if traffic is None else round(traffic),
+                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                "kernel": "klein_exact_kernel" if args.exact_order else "klein_mfma_kernel",
                 "kernel_ms_avg": round(k_avg_s * 1e3, 3), "units_per_launch": units,
-                "bytes_per_unit": b_alg(d),
-                "fp64_tflops": round(units * d * d / k_avg_s / 1e12, 3)}
+                "flops_per_unit": d * d,
+                "hbm_algorithmic": {"bytes_per_unit": b_alg(d),
+                                    "achieved_GBs": round(units * b_alg(d) / k_avg_s / 1e9, 1),
+                                    "frac_of_8TBs": round(units * b_alg(d) / k_avg_s / 1e9 / HBM_PEAK_GBS, 3)}}
     gemm = None
     if g_n:
         # B z over all proposals + the carried states: 2 d^2 flops per vector

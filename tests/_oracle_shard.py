@@ -1,0 +1,21 @@
+"""Test helper: an oracle-backed per-rank compute for lgs_amd.distributed (CPU, gloo)."""
+from typing import Optional
+
+import numpy as np
+
+from lgs_amd.distributed import ShardResult
+
+
+def oracle_compute_factory(oracle, R, cp, B, sigma, seed, *, thin: int = 1, mode: int = 0,
+                           center: Optional[np.ndarray] = None):
+    """CPU stand-in for `gpu_compute` (the oracle module is passed in by the test)."""
+    d = R.shape[0]
+
+    def compute(first_chain, n_chains, first_step, n_steps):
+        st = oracle.imhk(R, cp, B, sigma, n_chains, n_steps, center=center, seed=seed,
+                         first_chain=first_chain, first_step=first_step, mode=mode, trace=True)
+        kept = st["trace"][:, thin - 1::thin].reshape(-1, d)
+        mom = np.concatenate([kept.sum(0), (kept * kept).sum(0)]).astype(np.int64)
+        return ShardResult(int(st["accepts"].sum()), mom, kept.shape[0])
+
+    return compute

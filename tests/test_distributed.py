@@ -1,0 +1,71 @@
+"""Multi-process path on CPU (gloo, world size 2): sharding + the single all-reduce.
+
+The per-rank compute is the oracle (test infrastructure); the GPU path uses the
+same `imhk_sharded` with `gpu_compute`.  The all-reduced statistics must equal a
+single-process run over all chains (counter-addressed draws make them
+bit-identical for any world size)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import golden_R, load_golden
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    for p in (os.path.join(repo, "lattice-gaussian-mcmc_amd"), os.path.join(repo, "oracle"), here):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import lgs_oracle
+    from lgs_amd.distributed import imhk_sharded
+    from _oracle_shard import oracle_compute_factory
+    from conftest import golden_R, load_golden
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = load_golden("klein_ntru32.npz")
+    R, cp, B = golden_R(g)
+    comp = oracle_compute_factory(lgs_oracle, R, cp, B, float(g["sigma"]), 4242, thin=2)
+    acc, mom, kept = imhk_sharded(comp, 7, 10, rank=rank, world=world)
+    out[rank] = (acc, mom.tolist(), kept)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_range_partitions():
+    from lgs_amd.distributed import shard_range
+    for n in (1, 7, 16, 1000):
+        for w in (1, 2, 3, 8):
+            parts = [shard_range(n, r, w) for r in range(w)]
+            assert sum(c for _, c in parts) == n
+            assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_matches_single_process(oracle):
+    from _oracle_shard import oracle_compute_factory
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    mp.start_processes(_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    g = load_golden("klein_ntru32.npz")
+    R, cp, B = golden_R(g)
+    single = oracle_compute_factory(oracle, R, cp, B, float(g["sigma"]), 4242, thin=2)(0, 7, 1, 10)
+    for rank in (0, 1):
+        acc, mom, kept = out[rank]
+        assert acc == single.accepts
+        assert kept == single.kept == 7 * 5
+        assert np.array_equal(np.array(mom), single.moments)
