@@ -42,8 +42,8 @@ def b_alg(d):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3_ntru512")
     ap.add_argument("--chains", type=int, default=1 << 14, help="IMHK chains per GPU")
     ap.add_argument("--imhk-steps", type=int, default=16, help="IMHK steps per bench step")
@@ -95,9 +95,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("LGS_ONE_DEVICE") == "1":  # rehearsal: every rank on device 0 (gloo)
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("LGS_DIST_BACKEND", "nccl")  # nccl = RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     lat, sigma = build_config(args.config)
@@ -132,8 +138,15 @@ def main():
                  v_samples=v_samples, moments=mom, flags=flags)
         step_counter[0] += T
 
+    def reduce_stats():
+        stats = torch.cat([acc.sum().reshape(1), mom])  # per-rank accumulators
+        if world > 1:
+            dist.all_reduce(stats)  # the single RCCL collective over xGMI
+        return stats
+
     for _ in range(args.warmup):
         one_step()
+    reduce_stats()  # warm torch's lazily loaded kernels and the communicator
     acc.zero_()
     mom.zero_()
     ctx.timing_enable(True)
@@ -143,9 +156,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
-    stats = torch.cat([acc.sum().reshape(1), mom])  # per-rank accumulators
-    if world > 1:
-        dist.all_reduce(stats)  # the single RCCL collective over xGMI
+    stats = reduce_stats()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
