@@ -72,7 +72,7 @@ struct Timer {
 
 struct BzCall {  // an int8-digit B z launch, replayed in fp64 if a digit overflowed
     const void* Z;
-    bool z64;
+    int zb;
     int64_t ldz, n;
     double* V;
     int64_t rb, rstride, roff;
@@ -89,7 +89,7 @@ struct lgs_ctx {
     double sigma = 0;
     int precision = 10;
     uint32_t basis_flags = 0;
-    int panel = 16;
+    int panel = 32;
     bool has_B = false;
     DevBuf R, RP, RC, BT, coord;  // coord: cp | rii | sig | sig_ref | lterm | irii | ros | isr
     DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
@@ -100,6 +100,7 @@ struct lgs_ctx {
     DevBuf Z, LW, V, sel, fsel, cnt, ccnt, flags, stage_a, stage_b, stage_c, stage_d, stage_e,
         stage_f, stage_g, vs;
     int64_t max_props = 1 << 18;
+    int zint = 4;  // internal coefficient store width (bytes); LGS_ZINT=2: 16-bit, sticky 32-bit on overflow
     // timing
     bool timing = false;
     double t_ms[4] = {0, 0, 0, 0};
@@ -223,39 +224,58 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
 }
 
 // Kernel choice: exact order on request; otherwise the MFMA far-field kernel when
-// the launch is whole waves with 16-B aligned coefficient rows (panel 16), else
-// the VALU panel kernel.  LGS_KERNEL=valu forces the VALU kernel.
-int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, bool z64, void* Z) {
+// the launch is whole waves with aligned coefficient rows, else the VALU panel
+// kernel.  LGS_KERNEL=valu|mfma|exact overrides.
+int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int zb, void* Z) {
     Scope s(c, 0);
-    static const bool force_valu = getenv("LGS_KERNEL") && strcmp(getenv("LGS_KERNEL"), "valu") == 0;
-    int panel = c->panel;
-    if (!exact && !force_valu && c->panel == 16 && a.n % 64 == 0 && a.ldz % 4 == 0 &&
-        ((uintptr_t)Z % 16) == 0)
-        panel = 0;
-    HIP_TRY(lgs::launch::klein(a, c->R.as<double>(), c->RP.as<double>(), c->RC.as<double>(), panel,
-                               exact, wl, z64, Z, c->stream));
+    static const char* force = getenv("LGS_KERNEL");
+    int kernel = lgs::kKernelValu;
+    if (exact || (force && strcmp(force, "exact") == 0))
+        kernel = lgs::kKernelExact;
+    else if (!(force && strcmp(force, "valu") == 0) && a.n % 64 == 0 && a.ldz % 4 == 0 &&
+             ((uintptr_t)Z % 16) == 0)
+        kernel = lgs::kKernelMfma;
+    HIP_TRY(lgs::launch::klein(a, c->R.as<double>(), c->RP.as<double>(), c->RC.as<double>(),
+                               c->panel, kernel, wl, zb, Z, c->stream));
     return LGS_OK;
+}
+
+// Klein launch into an internal coefficient store of width zb.  A 16-bit store
+// that overflowed (|z| > 32767) is redone at 32 bits -- same counters, same
+// samples -- and the context stays at 32 bits from then on.
+int run_klein_store(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int& zb, void* Z) {
+    int rc = run_klein(c, a, exact, wl, zb, Z);
+    if (rc || zb != 2) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    unsigned int f = 0;
+    HIP_TRY(hipMemcpy(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost));
+    if (!(f & lgs::kFlagOverflow16)) return LGS_OK;
+    f &= ~lgs::kFlagOverflow16;
+    HIP_TRY(hipMemcpy(c->flags.p, &f, sizeof(f), hipMemcpyHostToDevice));
+    c->zint = 4;
+    zb = 4;
+    return run_klein(c, a, exact, wl, zb, Z);
 }
 
 int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
     Scope s(c, 1);
-    HIP_TRY(lgs::launch::bz(b.Z, b.z64, b.ldz, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
+    HIP_TRY(lgs::launch::bz(b.Z, b.zb, b.ldz, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
                             b.rstride, b.roff, c->stream));
     return LGS_OK;
 }
 
 // v = B z: exact int8-digit MFMA kernel for integer bases (fp64 replay on digit
 // overflow, see finish()), fp64 MFMA kernel otherwise.  LGS_BZ_FP64=1 forces fp64.
-int run_bz(lgs_ctx* c, const void* Z, bool z64, int64_t ldz, int64_t n, double* V,
+int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
            int64_t rb = 0, int64_t rstride = 0, int64_t roff = 0) {
     if (!c->has_B) return fail(LGS_ERR_STATE, "lattice points need B (lgs_set_basis B != NULL)");
-    BzCall b{Z, z64, ldz, n, V, rb > 0 ? rb : n, rstride, roff};
+    BzCall b{Z, zb, ldz, n, V, rb > 0 ? rb : n, rstride, roff};
     static const bool force64 = getenv("LGS_BZ_FP64") && atoi(getenv("LGS_BZ_FP64")) == 1;
     if (!c->has_Bi8 || force64) return run_bz_fp64(c, b);
     Scope s(c, 1);
     const int8_t* hi = c->Bd.as<int8_t>();
     const int8_t* lo = hi + (size_t)c->bd_rows * c->bd_cols;
-    HIP_TRY(lgs::launch::bz_i8(Z, z64, ldz, hi, lo, (int)c->bd_cols, (int)c->d, n, V, c->d, b.rb,
+    HIP_TRY(lgs::launch::bz_i8(Z, zb, ldz, hi, lo, (int)c->bd_cols, (int)c->d, n, V, c->d, b.rb,
                                b.rstride, b.roff, c->flags.as<unsigned int>(), c->stream));
     c->pending_i8.push_back(b);
     return LGS_OK;
@@ -291,7 +311,8 @@ int lgs_create(lgs_ctx** out, int device) {
         return fail(LGS_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
     c->stream = c->own;
-    if (const char* p = getenv("LGS_PANEL")) c->panel = atoi(p) == 32 ? 32 : 16;
+    if (const char* p = getenv("LGS_PANEL")) c->panel = atoi(p) == 16 ? 16 : 32;
+    if (const char* z = getenv("LGS_ZINT")) c->zint = atoi(z) == 2 ? 2 : 4;
     if (const char* m = getenv("LGS_MAX_PROPOSALS")) {
         long long v = atoll(m);
         if (v >= 64) c->max_props = v;
@@ -435,15 +456,17 @@ int lgs_klein(lgs_ctx* c, uint64_t seed, uint64_t first, int64_t n, void* z_out,
                wl = flags & LGS_WANG_LING;
     if (v_out && !c->has_B) return fail(LGS_ERR_STATE, "v_out requires B");
     const int64_t d = c->d;
-    const size_t zb = z64 ? 8 : 4;
+    const int ob = z64 ? 8 : 4;  // caller's coefficient width
     if ((rc = reset_flags(c))) return rc;
     const int64_t chunk = std::min<int64_t>(n, c->max_props);
-    // direct device coordinate-major output: the kernel writes straight into z_out
+    // direct device coordinate-major output: the kernel writes straight into z_out;
+    // otherwise an internal store (16-bit unless int64 / coordinate-major output)
     const bool direct = dev && cm && z_out;
-    if (!direct && (rc = c->Z.reserve((size_t)chunk * d * zb))) return rc;
+    int zb = (direct || ob == 8 || (z_out && cm)) ? ob : c->zint;
+    if (!direct && (rc = c->Z.reserve((size_t)chunk * d * std::max(zb, 4)))) return rc;
     if ((rc = c->LW.reserve((size_t)chunk * 8))) return rc;
     if (!dev) {
-        if (z_out && (rc = c->stage_a.reserve((size_t)chunk * d * zb))) return rc;
+        if (z_out && (rc = c->stage_a.reserve((size_t)chunk * d * ob))) return rc;
         if (v_out && (rc = c->V.reserve((size_t)chunk * d * 8))) return rc;
     }
     for (int64_t off = 0; off < n; off += chunk) {
@@ -454,31 +477,31 @@ int lgs_klein(lgs_ctx* c, uint64_t seed, uint64_t first, int64_t n, void* z_out,
         a.n = m;
         void* Zp;
         if (direct) {
-            Zp = (char*)z_out + (size_t)off * zb;
+            Zp = (char*)z_out + (size_t)off * ob;
             a.ldz = n;
         } else {
             Zp = c->Z.p;
             a.ldz = m;
         }
         a.LW = logw_out ? (dev ? logw_out + off : c->LW.as<double>()) : nullptr;
-        if ((rc = run_klein(c, a, exact, wl, z64, Zp))) return rc;
+        if ((rc = run_klein_store(c, a, exact, wl, zb, Zp))) return rc;
         if (z_out && !direct) {
-            if (cm) {  // coordinate-major output with host pointers or via staging
+            if (cm) {  // coordinate-major output through host pointers (zb == ob)
                 for (int64_t i = 0; i < d; ++i)
-                    HIP_TRY(hipMemcpy2DAsync((char*)z_out + ((size_t)i * n + off) * zb, 0,
-                                             (char*)Zp + (size_t)i * m * zb, 0, m * zb, 1,
+                    HIP_TRY(hipMemcpy2DAsync((char*)z_out + ((size_t)i * n + off) * ob, 0,
+                                             (char*)Zp + (size_t)i * m * ob, 0, m * ob, 1,
                                              kind_of(dev, true), c->stream));
             } else {
-                void* dst = dev ? (char*)z_out + (size_t)off * d * zb : c->stage_a.p;
-                HIP_TRY(lgs::launch::transpose_out(Zp, z64, a.ldz, m, (int)d, dst, z64, c->stream));
+                void* dst = dev ? (char*)z_out + (size_t)off * d * ob : c->stage_a.p;
+                HIP_TRY(lgs::launch::transpose_out(Zp, zb, a.ldz, m, (int)d, dst, ob, c->stream));
                 if (!dev)
-                    HIP_TRY(hipMemcpyAsync((char*)z_out + (size_t)off * d * zb, dst, (size_t)m * d * zb,
+                    HIP_TRY(hipMemcpyAsync((char*)z_out + (size_t)off * d * ob, dst, (size_t)m * d * ob,
                                            hipMemcpyDeviceToHost, c->stream));
             }
         }
         if (v_out) {
             double* V = dev ? v_out + (size_t)off * d : c->V.as<double>();
-            if ((rc = run_bz(c, Zp, z64, a.ldz, m, V))) return rc;
+            if ((rc = run_bz(c, Zp, zb, a.ldz, m, V))) return rc;
             if ((rc = settle_bz(c))) return rc;
             if (!dev)
                 HIP_TRY(hipMemcpyAsync(v_out + (size_t)off * d, V, (size_t)m * d * 8,
@@ -501,7 +524,7 @@ int lgs_lattice_points(lgs_ctx* c, int64_t n, const void* z, double* v_out, uint
     if (!z || !v_out) return fail(LGS_ERR_INVALID, "null buffer");
     const bool dev = flags & LGS_DEVICE_PTRS, z64 = flags & LGS_Z64, cm = flags & LGS_COORD_MAJOR;
     const int64_t d = c->d;
-    const size_t zb = z64 ? 8 : 4;
+    const int zb = z64 ? 8 : 4;
     if ((rc = reset_flags(c))) return rc;
     const void* Zc = z;
     if (!dev || !cm) {
@@ -515,7 +538,7 @@ int lgs_lattice_points(lgs_ctx* c, int64_t n, const void* z, double* v_out, uint
         if (cm) {
             Zc = src;
         } else {
-            HIP_TRY(lgs::launch::to_coord_major(src, z64, n, (int)d, c->Z.p, z64, n, c->stream));
+            HIP_TRY(lgs::launch::to_coord_major(src, zb, n, (int)d, c->Z.p, zb, n, c->stream));
             Zc = c->Z.p;
         }
     }
@@ -524,7 +547,7 @@ int lgs_lattice_points(lgs_ctx* c, int64_t n, const void* z, double* v_out, uint
         if ((rc = c->V.reserve((size_t)n * d * 8))) return rc;
         V = c->V.as<double>();
     }
-    if ((rc = run_bz(c, Zc, z64, n, n, V))) return rc;
+    if ((rc = run_bz(c, Zc, zb, n, n, V))) return rc;
     if ((rc = settle_bz(c))) return rc;
     if (!dev) HIP_TRY(hipMemcpyAsync(v_out, V, (size_t)n * d * 8, hipMemcpyDeviceToHost, c->stream));
     return finish(c);
@@ -537,7 +560,7 @@ int lgs_log_density(lgs_ctx* c, int64_t n, const void* z, double* out, uint32_t 
     if (!z || !out) return fail(LGS_ERR_INVALID, "null buffer");
     const bool dev = flags & LGS_DEVICE_PTRS, z64 = flags & LGS_Z64, cm = flags & LGS_COORD_MAJOR;
     const int64_t d = c->d;
-    const size_t zb = z64 ? 8 : 4;
+    const int zb = z64 ? 8 : 4;
     if ((rc = reset_flags(c))) return rc;
     const void* Zc = z;
     if (!dev || !cm) {
@@ -551,7 +574,7 @@ int lgs_log_density(lgs_ctx* c, int64_t n, const void* z, double* out, uint32_t 
         if (cm) {
             Zc = src;
         } else {
-            HIP_TRY(lgs::launch::to_coord_major(src, z64, n, (int)d, c->Z.p, z64, n, c->stream));
+            HIP_TRY(lgs::launch::to_coord_major(src, zb, n, (int)d, c->Z.p, zb, n, c->stream));
             Zc = c->Z.p;
         }
     }
@@ -563,7 +586,7 @@ int lgs_log_density(lgs_ctx* c, int64_t n, const void* z, double* out, uint32_t 
     lgs::KleinArgs a = base_args(c, 0);
     a.n = n;
     a.ldz = n;
-    HIP_TRY(lgs::launch::log_density(a, c->R.as<double>(), Zc, z64, o, c->stream));
+    HIP_TRY(lgs::launch::log_density(a, c->R.as<double>(), Zc, zb, o, c->stream));
     if (!dev) HIP_TRY(hipMemcpyAsync(out, o, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
     return finish(c);
 }
@@ -590,7 +613,8 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
     if (first_chain + (uint64_t)nc > (1ull << 32) || first_step + (uint64_t)n_steps > (1ull << 32))
         return fail(LGS_ERR_INVALID, "chain / step counters must stay below 2^32");
     const int64_t d = c->d;
-    const size_t zb = z64 ? 8 : 4;
+    const int ob = z64 ? 8 : 4;      // caller's coefficient width (z_state, z_samples)
+    int zb = z64 ? 8 : c->zint;      // internal proposal store width
     const int64_t n_keep = n_steps / thin;
     if ((rc = reset_flags(c))) return rc;
 
@@ -600,7 +624,7 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
     T = std::min<int64_t>(T, std::max<int64_t>(n_steps, 1));
     const int64_t np = nc * T;
     const int64_t kmax = std::max<int64_t>(T / thin, 1);
-    if ((rc = c->Z.reserve((size_t)np * d * zb)) || (rc = c->LW.reserve((size_t)np * 8)) ||
+    if ((rc = c->Z.reserve((size_t)np * d * std::max(zb, 4))) || (rc = c->LW.reserve((size_t)np * 8)) ||
         (rc = c->sel.reserve((size_t)std::max<int64_t>(nc * kmax, nc) * 8)) ||
         (rc = c->fsel.reserve((size_t)nc * 8)) || (rc = c->cnt.reserve((size_t)np * 4)) ||
         (rc = c->ccnt.reserve((size_t)nc * 4)))
@@ -616,14 +640,14 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         HIP_TRY(hipMemcpyAsync(h_init.data(), state_init, nc * 4, hipMemcpyDeviceToHost, c->stream));
     } else {
         memcpy(h_init.data(), state_init, nc * 4);
-        if ((rc = c->stage_a.reserve((size_t)nc * d * zb)) || (rc = c->stage_b.reserve((size_t)nc * 8)) ||
+        if ((rc = c->stage_a.reserve((size_t)nc * d * ob)) || (rc = c->stage_b.reserve((size_t)nc * 8)) ||
             (rc = c->stage_c.reserve((size_t)nc * 4)) || (rc = c->stage_d.reserve((size_t)nc * 8)))
             return rc;
         zs = c->stage_a.p;
         lws = c->stage_b.as<double>();
         init = c->stage_c.as<int32_t>();
         acc = c->stage_d.as<int64_t>();
-        HIP_TRY(hipMemcpyAsync(zs, z_state, (size_t)nc * d * zb, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(zs, z_state, (size_t)nc * d * ob, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(lws, logw_state, nc * 8, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(init, state_init, nc * 4, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(acc, accepts, nc * 8, hipMemcpyHostToDevice, c->stream));
@@ -652,11 +676,11 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         a.n = nc;
         a.ldz = nc;
         a.LW = c->LW.as<double>();
-        if ((rc = run_klein(c, a, exact, wl, z64, c->Z.p))) return rc;
+        if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p))) return rc;
         std::vector<int64_t> s(nc);
         for (int64_t i = 0; i < nc; ++i) s[i] = h_init[i] ? -1 : i;
         HIP_TRY(hipMemcpyAsync(c->sel.p, s.data(), nc * 8, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(lgs::launch::gather_z(c->Z.p, z64, nc, c->sel.as<int64_t>(), nc, 1, zs, cm, nc,
+        HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, nc, c->sel.as<int64_t>(), nc, 1, zs, ob, cm, nc,
                                       (int)d, zs, cm, c->stream));
         std::vector<double> h_lw(nc), cur(nc);
         HIP_TRY(hipMemcpyAsync(h_lw.data(), c->LW.p, nc * 8, hipMemcpyDeviceToHost, c->stream));
@@ -685,7 +709,7 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         a.n = npb;
         a.ldz = npb;
         a.LW = c->LW.as<double>();
-        if ((rc = run_klein(c, a, exact, wl, z64, c->Z.p))) return rc;
+        if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p))) return rc;
         if (moments) HIP_TRY(hipMemsetAsync(c->cnt.p, 0, (size_t)npb * 4, c->stream));
         lgs::AcceptArgs aa{};
         aa.nc = nc;
@@ -708,36 +732,36 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         }
         if (moments) {
             Scope s(c, 3);
-            HIP_TRY(lgs::launch::moments(c->Z.p, z64, npb, c->cnt.as<int32_t>(), npb, (int)d, mom, c->stream));
-            HIP_TRY(lgs::launch::moments_carry(zs, z64, cm, nc, (int)d, c->ccnt.as<int32_t>(), mom, c->stream));
+            HIP_TRY(lgs::launch::moments(c->Z.p, zb, npb, c->cnt.as<int32_t>(), npb, (int)d, mom, c->stream));
+            HIP_TRY(lgs::launch::moments_carry(zs, ob, cm, nc, (int)d, c->ccnt.as<int32_t>(), mom, c->stream));
         }
         if ((z_samples || v_samples) && kb > 0) {
             // kept states q = chain*kb + k, gathered coordinate-major (d x nq); chain-major
             // proposal order makes this a near-contiguous copy
             const int64_t nq = nc * kb;
-            if ((rc = c->stage_f.reserve((size_t)nq * d * zb))) return rc;
-            HIP_TRY(lgs::launch::gather_z(c->Z.p, z64, npb, c->sel.as<int64_t>(), nq, kb, zs, cm, nc,
+            if ((rc = c->stage_f.reserve((size_t)nq * d * ob))) return rc;
+            HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, npb, c->sel.as<int64_t>(), nq, kb, zs, ob, cm, nc,
                                           (int)d, c->stage_f.p, 1, c->stream));
             if (v_samples) {  // rows (chain, first_keep + k) of the n_chains x n_keep x d output
-                if ((rc = run_bz(c, c->stage_f.p, z64, nq, nq, v_samples, kb, n_keep, first_keep)))
+                if ((rc = run_bz(c, c->stage_f.p, ob, nq, nq, v_samples, kb, n_keep, first_keep)))
                     return rc;
             }
             if (z_samples) {
-                if ((rc = c->stage_g.reserve((size_t)nq * d * zb))) return rc;
-                HIP_TRY(lgs::launch::transpose_out(c->stage_f.p, z64, nq, nq, (int)d, c->stage_g.p,
-                                                   z64, c->stream));
-                HIP_TRY(hipMemcpy2DAsync((char*)z_samples + (size_t)first_keep * d * zb,
-                                         (size_t)n_keep * d * zb, c->stage_g.p, (size_t)kb * d * zb,
-                                         (size_t)kb * d * zb, nc, kind_of(dev, true), c->stream));
+                if ((rc = c->stage_g.reserve((size_t)nq * d * ob))) return rc;
+                HIP_TRY(lgs::launch::transpose_out(c->stage_f.p, ob, nq, nq, (int)d, c->stage_g.p,
+                                                   ob, c->stream));
+                HIP_TRY(hipMemcpy2DAsync((char*)z_samples + (size_t)first_keep * d * ob,
+                                         (size_t)n_keep * d * ob, c->stage_g.p, (size_t)kb * d * ob,
+                                         (size_t)kb * d * ob, nc, kind_of(dev, true), c->stream));
             }
         }
         // chain states after the block (in place; carried chains keep their row)
-        HIP_TRY(lgs::launch::gather_z(c->Z.p, z64, npb, c->fsel.as<int64_t>(), nc, 1, zs, cm, nc,
+        HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, npb, c->fsel.as<int64_t>(), nc, 1, zs, ob, cm, nc,
                                       (int)d, zs, cm, c->stream));
         if ((rc = finish(c))) return rc;
     }
     if (!dev) {
-        HIP_TRY(hipMemcpyAsync(z_state, zs, (size_t)nc * d * zb, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(z_state, zs, (size_t)nc * d * ob, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemcpyAsync(logw_state, lws, nc * 8, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemcpyAsync(state_init, init, nc * 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemcpyAsync(accepts, acc, nc * 8, hipMemcpyDeviceToHost, c->stream));

@@ -9,6 +9,11 @@ namespace lgs {
 constexpr unsigned int kFlagNonFinite = 1u;  // a conditional mean was NaN/inf
 constexpr unsigned int kFlagOverflow = 2u;   // |z| >= 2^31 with an int32 store
 constexpr unsigned int kFlagI8Range = 4u;    // |z| > 32639: int8-digit B z must be redone in fp64
+constexpr unsigned int kFlagOverflow16 = 8u; // |z| > 32767 in a 16-bit internal store
+
+constexpr int kKernelExact = 0;  // reference-order back-substitution
+constexpr int kKernelValu = 1;   // blocked panel kernel, VALU far field
+constexpr int kKernelMfma = 2;   // blocked panel kernel, fp64 MFMA far field
 
 // Per-launch arguments of the Klein samplers.  Per-coordinate arrays (length d):
 //   cp      c' = Q^T c
@@ -62,31 +67,32 @@ struct AcceptArgs {
 };
 
 namespace launch {
+// zb / ob / ib: coefficient element width in bytes (2, 4 or 8)
 hipError_t klein(const KleinArgs& a, const double* R, const double* RP, const double* RC,
-                 int panel, bool exact, bool wl, bool z64, void* Z, hipStream_t st);
+                 int panel, int kernel, bool wl, int zb, void* Z, hipStream_t st);
 hipError_t accept(const AcceptArgs& a, hipStream_t st);
 hipError_t samplez_probe(const double* mu, const double* sig, const double* u, int64_t n,
                          int precision, int linear, int force_table, int64_t* z, double* ln,
                          hipStream_t st);
-hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, bool z64, double* out,
+hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, int zb, double* out,
                        hipStream_t st);
-hipError_t moments(const void* Z, bool z64, int64_t ldz, const int32_t* cnt, int64_t n, int d,
+hipError_t moments(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int d,
                    unsigned long long* mom, hipStream_t st);
-hipError_t moments_carry(const void* zs, bool z64, int coord_major, int64_t nc, int d,
+hipError_t moments_carry(const void* zs, int zb, int coord_major, int64_t nc, int d,
                          const int32_t* cc, unsigned long long* mom, hipStream_t st);
-hipError_t gather_z(const void* Z, bool z64, int64_t ldz, const int64_t* sel, int64_t nq,
-                    int64_t q_per_chain, const void* zs, int zs_coord_major, int64_t nc, int d,
-                    void* out, int out_coord_major, hipStream_t st);
+hipError_t gather_z(const void* Z, int zb, int64_t ldz, const int64_t* sel, int64_t nq,
+                    int64_t q_per_chain, const void* zs, int ob, int zs_coord_major, int64_t nc,
+                    int d, void* out, int out_coord_major, hipStream_t st);
 hipError_t gather_v(const double* V, const int64_t* sel, int64_t nq, int64_t q_per_chain,
                     const double* vs, int d, double* out, hipStream_t st);
-hipError_t transpose_out(const void* Z, bool z64, int64_t ldz, int64_t n, int d, void* out,
-                         bool out64, hipStream_t st);
-hipError_t to_coord_major(const void* in, bool in64, int64_t n, int d, void* Z, bool z64,
-                          int64_t ldz, hipStream_t st);
+hipError_t transpose_out(const void* Z, int zb, int64_t ldz, int64_t n, int d, void* out, int ob,
+                         hipStream_t st);
+hipError_t to_coord_major(const void* in, int ib, int64_t n, int d, void* Z, int zb, int64_t ldz,
+                          hipStream_t st);
 // V row of sample s: (s / rb) * rstride + roff + s % rb (rb = n, rstride = roff = 0: row s)
-hipError_t bz(const void* Z, bool z64, int64_t ldz, const double* BT, int d, int64_t n, double* V,
+hipError_t bz(const void* Z, int zb, int64_t ldz, const double* BT, int d, int64_t n, double* V,
               int64_t ldv, int64_t rb, int64_t rstride, int64_t roff, hipStream_t st);
-hipError_t bz_i8(const void* Z, bool z64, int64_t ldz, const int8_t* Bd1, const int8_t* Bd0, int dc,
+hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int8_t* Bd1, const int8_t* Bd0, int dc,
                  int d, int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, hipStream_t st);
 }  // namespace launch

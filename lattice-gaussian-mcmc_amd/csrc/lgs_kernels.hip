@@ -74,6 +74,7 @@ __device__ __forceinline__ int64_t decide_coord(const KleinArgs& a, int i, doubl
 template <typename ZT>
 __device__ __forceinline__ void store_z(ZT* Z, size_t off, int64_t zi, unsigned int& flags) {
     if (sizeof(ZT) == 4 && (zi > 2147483647LL || zi < -2147483648LL)) flags |= kFlagOverflow;
+    if (sizeof(ZT) == 2 && (zi > 32767 || zi < -32768)) flags |= kFlagOverflow16;
     Z[off] = (ZT)zi;
 }
 
@@ -168,12 +169,13 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
 }
 
 // ------------------------------------------------------------ panel, MFMA far field
-// Same sampler and panel layout (PB = 16) as klein_panel_kernel, but the
-// far-field product of a panel -- F[16 rows][64 chains] = R_panel[16 x K] *
+// Same sampler and panel layout as klein_panel_kernel (PB = 16 or 32 rows), but
+// the far-field product of a panel -- F[PB rows][64 chains] = R_panel[PB x K] *
 // X[K x 64 chains], K = d - p_hi -- runs on the matrix cores of the wave:
-// v_mfma_f64_16x16x4_f64 with A = R tile (lane l: R[p_lo + (l&15)][j0 + (l>>4)],
-// one coalesced 512-B load) and B = coefficients (lane l loads 4 consecutive
-// chains of row j0 + (l>>4) as one 16-B load; MFMA g takes chain 4n+g, n = l&15).
+// v_mfma_f64_16x16x4_f64, one 16-row tile t per MFMA, A = R tile (lane l:
+// R[p_lo + 16t + (l&15)][j0 + (l>>4)], coalesced 512 B) and B = coefficients
+// (lane l loads 4 consecutive chains of row j0 + (l>>4) in one load; MFMA g takes
+// chain 4n+g, n = l&15), so one coefficient load feeds PB/16 * 4 MFMAs.
 // D (lane l: rows (l>>4)+4*reg, chain 4*(l&15)+g) is transposed to one chain per
 // lane through a per-wave 8 KB LDS tile; the near field and SampleZ then run on
 // the VALU exactly as in klein_panel_kernel.  Requires n % 64 == 0, ldz % 4 == 0.
@@ -182,13 +184,34 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
 typedef int v4i32_t __attribute__((ext_vector_type(4)));
 typedef double d4_t __attribute__((ext_vector_type(4)));
 
-template <typename ZT, bool WL>
-__global__ __launch_bounds__(256, 3) void klein_mfma_kernel(const KleinArgs a,
-                                                         const double* __restrict__ RP,
-                                                         const double* __restrict__ RC,
-                                                         ZT* __restrict__ Z) {
-    constexpr int PB = 16, LDF = 65;  // LDS tile pitch (doubles): conflict-free row reads
-    __shared__ double Fl[4][PB * LDF];
+template <typename ZT>
+__device__ __forceinline__ v4i32_t load4_nt(const ZT* p) {
+    v4i32_t v;
+    if constexpr (sizeof(ZT) == 2) {
+        const unsigned long long w = __builtin_nontemporal_load((const unsigned long long*)p);
+        v[0] = (int)(short)(w & 0xffff);
+        v[1] = (int)(short)((w >> 16) & 0xffff);
+        v[2] = (int)(short)((w >> 32) & 0xffff);
+        v[3] = (int)(short)(w >> 48);
+    } else if constexpr (sizeof(ZT) == 4) {
+        v = __builtin_nontemporal_load((const v4i32_t*)p);
+    } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) v[g] = (int)__builtin_nontemporal_load(p + g);
+    }
+    return v;
+}
+
+template <typename ZT, int PB, bool WL>
+#ifndef LGS_MFMA_LB32
+#define LGS_MFMA_LB32 2
+#endif
+__global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_kernel(const KleinArgs a,
+                                                            const double* __restrict__ RP,
+                                                            const double* __restrict__ RC,
+                                                            ZT* __restrict__ Z) {
+    constexpr int NT = PB / 16, LDF = 65;  // LDS tile pitch (doubles): conflict-free row reads
+    __shared__ double Fl[4][16 * LDF];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t p0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
     if (p0 >= a.n) return;  // whole waves only (n % 64 == 0)
@@ -217,50 +240,57 @@ __global__ __launch_bounds__(256, 3) void klein_mfma_kernel(const KleinArgs a,
             // stored by this wave's lanes in earlier panels
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            d4_t f[4];
+            d4_t f[NT][4];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) f[g] = (d4_t){0.0, 0.0, 0.0, 0.0};
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) f[t][g] = (d4_t){0.0, 0.0, 0.0, 0.0};
             const double* __restrict__ rp = RP + (size_t)PB * PB * ((size_t)pk * (pk - 1) / 2);
             const ZT* zcol = Z + p0 + 4 * nq;
             // software pipeline, 4 stages: the loads of step j0+16 are issued while
             // the MFMAs of step j0 run (VMEM returns in order, so each wait is a
             // counted vmcnt); K = d - p_hi is a multiple of 16
-            double ra[4];
+            double ra[4][NT];
             v4i32_t zb[4];
-            auto load_stage = [&](int jj, double& av, v4i32_t& zv) {
-                av = rp[(size_t)(jj - p_hi + kq) * PB + nq];
-                const ZT* zr = zcol + (size_t)(jj + kq) * ldz;
-                if (sizeof(ZT) == 4) {
-                    zv = __builtin_nontemporal_load((const v4i32_t*)zr);
-                } else {
+            auto load_stage = [&](int jj, double (&av)[NT], v4i32_t& zv) {
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) zv[g] = (int)__builtin_nontemporal_load(zr + g);
-                }
+                for (int t = 0; t < NT; ++t) av[t] = rp[(size_t)(jj - p_hi + kq) * PB + 16 * t + nq];
+                zv = load4_nt(zcol + (size_t)(jj + kq) * ldz);
             };
 #pragma unroll
             for (int st = 0; st < 4; ++st) load_stage(p_hi + 4 * st, ra[st], zb[st]);
             for (int j0 = p_hi; j0 < d; j0 += 16) {
 #pragma unroll
                 for (int st = 0; st < 4; ++st) {
-                    const double a_cur = ra[st];
+                    double a_cur[NT];
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) a_cur[t] = ra[st][t];
                     const v4i32_t z_cur = zb[st];
                     const int jn = j0 + 16 + 4 * st;
                     if (jn < d) load_stage(jn, ra[st], zb[st]);
 #pragma unroll
-                    for (int g = 0; g < 4; ++g)
-                        f[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur, (double)z_cur[g], f[g], 0, 0, 0);
+                    for (int g = 0; g < 4; ++g) {
+                        const double bz = (double)z_cur[g];
+#pragma unroll
+                        for (int t = 0; t < NT; ++t)
+                            f[t][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[t], bz, f[t][g], 0, 0, 0);
+                    }
                 }
             }
-            // D -> LDS [row][chain] -> one chain per lane
+            // D -> LDS [row][chain] -> one chain per lane, one 16-row tile at a time
 #pragma unroll
-            for (int g = 0; g < 4; ++g)
+            for (int t = 0; t < NT; ++t) {
 #pragma unroll
-                for (int reg = 0; reg < 4; ++reg) F[(kq + 4 * reg) * LDF + 4 * nq + g] = f[g][reg];
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
+                for (int g = 0; g < 4; ++g)
 #pragma unroll
-            for (int r = 0; r < PB; ++r) acc[r] = F[r * LDF + lane];
-            __builtin_amdgcn_wave_barrier();
+                    for (int reg = 0; reg < 4; ++reg) F[(kq + 4 * reg) * LDF + 4 * nq + g] = f[t][g][reg];
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[16 * t + r] = F[r * LDF + lane];
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
         } else {
 #pragma unroll
             for (int r = 0; r < PB; ++r) acc[r] = 0.0;
@@ -716,51 +746,62 @@ __global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z,
 // ============================================================ launchers
 namespace launch {
 
-template <typename ZT>
-static hipError_t klein_t(const KleinArgs& a, const double* R, const double* RP, const double* RC,
-                          int panel, bool exact, bool wl, void* Z, hipStream_t st) {
-    const dim3 block(256);
-    const dim3 grid((unsigned)((a.n + 255) / 256));
-    ZT* z = (ZT*)Z;
-    if (!exact && panel == 0) {  // MFMA far field (panel rows fixed at 16)
+// element type dispatch on the coefficient width in bytes (2, 4, 8)
+#define LGS_ZT(zb, T, ...)                 \
+    do {                                   \
+        if ((zb) == 2) {                   \
+            using T = int16_t;             \
+            __VA_ARGS__;                   \
+        } else if ((zb) == 4) {            \
+            using T = int32_t;             \
+            __VA_ARGS__;                   \
+        } else {                           \
+            using T = int64_t;             \
+            __VA_ARGS__;                   \
+        }                                  \
+    } while (0)
+
+template <typename ZT, int PB>
+static void klein_pb(const KleinArgs& a, const double* RP, const double* RC, int kernel, bool wl,
+                     ZT* z, dim3 grid, hipStream_t st) {
+    if (kernel == kKernelMfma) {
         if (wl)
-            hipLaunchKernelGGL((klein_mfma_kernel<ZT, true>), grid, block, 0, st, a, RP, RC, z);
+            hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, true>), grid, dim3(256), 0, st, a, RP, RC, z);
         else
-            hipLaunchKernelGGL((klein_mfma_kernel<ZT, false>), grid, block, 0, st, a, RP, RC, z);
-    } else if (exact) {
-        if (wl)
-            hipLaunchKernelGGL((klein_exact_kernel<ZT, true>), grid, block, 0, st, a, R, z);
-        else
-            hipLaunchKernelGGL((klein_exact_kernel<ZT, false>), grid, block, 0, st, a, R, z);
-    } else if (panel == 16) {
-        if (wl)
-            hipLaunchKernelGGL((klein_panel_kernel<ZT, 16, true>), grid, block, 0, st, a, RP, RC, z);
-        else
-            hipLaunchKernelGGL((klein_panel_kernel<ZT, 16, false>), grid, block, 0, st, a, RP, RC, z);
+            hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, false>), grid, dim3(256), 0, st, a, RP, RC, z);
     } else {
         if (wl)
-            hipLaunchKernelGGL((klein_panel_kernel<ZT, 32, true>), grid, block, 0, st, a, RP, RC, z);
+            hipLaunchKernelGGL((klein_panel_kernel<ZT, PB, true>), grid, dim3(256), 0, st, a, RP, RC, z);
         else
-            hipLaunchKernelGGL((klein_panel_kernel<ZT, 32, false>), grid, block, 0, st, a, RP, RC, z);
+            hipLaunchKernelGGL((klein_panel_kernel<ZT, PB, false>), grid, dim3(256), 0, st, a, RP, RC, z);
     }
-    return hipGetLastError();
 }
 
 hipError_t klein(const KleinArgs& a, const double* R, const double* RP, const double* RC,
-                 int panel, bool exact, bool wl, bool z64, void* Z, hipStream_t st) {
+                 int panel, int kernel, bool wl, int zb, void* Z, hipStream_t st) {
     if (a.n <= 0) return hipSuccess;
-    return z64 ? klein_t<int64_t>(a, R, RP, RC, panel, exact, wl, Z, st)
-               : klein_t<int32_t>(a, R, RP, RC, panel, exact, wl, Z, st);
+    const dim3 grid((unsigned)((a.n + 255) / 256));
+    LGS_ZT(zb, ZT, {
+        ZT* z = (ZT*)Z;
+        if (kernel == kKernelExact) {
+            if (wl)
+                hipLaunchKernelGGL((klein_exact_kernel<ZT, true>), grid, dim3(256), 0, st, a, R, z);
+            else
+                hipLaunchKernelGGL((klein_exact_kernel<ZT, false>), grid, dim3(256), 0, st, a, R, z);
+        } else if (panel == 32) {
+            klein_pb<ZT, 32>(a, RP, RC, kernel, wl, z, grid, st);
+        } else {
+            klein_pb<ZT, 16>(a, RP, RC, kernel, wl, z, grid, st);
+        }
+    });
+    return hipGetLastError();
 }
 
-hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, bool z64, double* out,
+hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, int zb, double* out,
                        hipStream_t st) {
     if (a.n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((a.n + 255) / 256));
-    if (z64)
-        hipLaunchKernelGGL(log_density_kernel<int64_t>, grid, dim3(256), 0, st, a, R, (const int64_t*)Z, out);
-    else
-        hipLaunchKernelGGL(log_density_kernel<int32_t>, grid, dim3(256), 0, st, a, R, (const int32_t*)Z, out);
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(log_density_kernel<ZT>, grid, dim3(256), 0, st, a, R, (const ZT*)Z, out));
     return hipGetLastError();
 }
 
@@ -779,37 +820,28 @@ hipError_t accept(const AcceptArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t moments(const void* Z, bool z64, int64_t ldz, const int32_t* cnt, int64_t n, int d,
+hipError_t moments(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int d,
                    unsigned long long* mom, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const int64_t chunk = 16384;
     const dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
-    if (z64)
-        hipLaunchKernelGGL(moments_kernel<int64_t>, grid, dim3(256), 0, st, (const int64_t*)Z, ldz, cnt, n, d, chunk, mom);
-    else
-        hipLaunchKernelGGL(moments_kernel<int32_t>, grid, dim3(256), 0, st, (const int32_t*)Z, ldz, cnt, n, d, chunk, mom);
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(moments_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, d, chunk, mom));
     return hipGetLastError();
 }
 
-hipError_t moments_carry(const void* zs, bool z64, int coord_major, int64_t nc, int d,
+hipError_t moments_carry(const void* zs, int zb, int coord_major, int64_t nc, int d,
                          const int32_t* cc, unsigned long long* mom, hipStream_t st) {
     if (nc <= 0) return hipSuccess;
-    if (z64)
-        hipLaunchKernelGGL(moments_carry_kernel<int64_t>, dim3(d), dim3(256), 0, st, (const int64_t*)zs, coord_major, nc, d, cc, mom);
-    else
-        hipLaunchKernelGGL(moments_carry_kernel<int32_t>, dim3(d), dim3(256), 0, st, (const int32_t*)zs, coord_major, nc, d, cc, mom);
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(moments_carry_kernel<ZT>, dim3(d), dim3(256), 0, st, (const ZT*)zs, coord_major, nc, d, cc, mom));
     return hipGetLastError();
 }
 
-hipError_t gather_z(const void* Z, bool z64, int64_t ldz, const int64_t* sel, int64_t nq,
-                    int64_t q_per_chain, const void* zs, int zs_coord_major, int64_t nc, int d,
-                    void* out, int out_coord_major, hipStream_t st) {
+hipError_t gather_z(const void* Z, int zb, int64_t ldz, const int64_t* sel, int64_t nq,
+                    int64_t q_per_chain, const void* zs, int ob, int zs_coord_major, int64_t nc,
+                    int d, void* out, int out_coord_major, hipStream_t st) {
     if (nq <= 0) return hipSuccess;
     const dim3 grid((unsigned)((nq + 255) / 256), (unsigned)d);
-    if (z64)
-        hipLaunchKernelGGL((gather_z_kernel<int64_t, int64_t>), grid, dim3(256), 0, st, (const int64_t*)Z, ldz, sel, nq, q_per_chain, (const int64_t*)zs, zs_coord_major, nc, d, (int64_t*)out, out_coord_major);
-    else
-        hipLaunchKernelGGL((gather_z_kernel<int32_t, int32_t>), grid, dim3(256), 0, st, (const int32_t*)Z, ldz, sel, nq, q_per_chain, (const int32_t*)zs, zs_coord_major, nc, d, (int32_t*)out, out_coord_major);
+    LGS_ZT(zb, ZT, LGS_ZT(ob, OT, hipLaunchKernelGGL((gather_z_kernel<ZT, OT>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, nq, q_per_chain, (const OT*)zs, zs_coord_major, nc, d, (OT*)out, out_coord_major)));
     return hipGetLastError();
 }
 
@@ -821,54 +853,36 @@ hipError_t gather_v(const double* V, const int64_t* sel, int64_t nq, int64_t q_p
     return hipGetLastError();
 }
 
-hipError_t transpose_out(const void* Z, bool z64, int64_t ldz, int64_t n, int d, void* out,
-                         bool out64, hipStream_t st) {
+hipError_t transpose_out(const void* Z, int zb, int64_t ldz, int64_t n, int d, void* out, int ob,
+                         hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
-    if (z64 && out64)
-        hipLaunchKernelGGL((transpose_kernel<int64_t, int64_t>), grid, dim3(256), 0, st, (const int64_t*)Z, ldz, n, d, (int64_t*)out);
-    else if (!z64 && out64)
-        hipLaunchKernelGGL((transpose_kernel<int32_t, int64_t>), grid, dim3(256), 0, st, (const int32_t*)Z, ldz, n, d, (int64_t*)out);
-    else if (!z64 && !out64)
-        hipLaunchKernelGGL((transpose_kernel<int32_t, int32_t>), grid, dim3(256), 0, st, (const int32_t*)Z, ldz, n, d, (int32_t*)out);
-    else
-        return hipErrorInvalidValue;
+    LGS_ZT(zb, ZT, LGS_ZT(ob, OT, hipLaunchKernelGGL((transpose_kernel<ZT, OT>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, n, d, (OT*)out)));
     return hipGetLastError();
 }
 
-hipError_t to_coord_major(const void* in, bool in64, int64_t n, int d, void* Z, bool z64,
-                          int64_t ldz, hipStream_t st) {
+hipError_t to_coord_major(const void* in, int ib, int64_t n, int d, void* Z, int zb, int64_t ldz,
+                          hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
-    if (z64 && in64)
-        hipLaunchKernelGGL((to_coord_major_kernel<int64_t, int64_t>), grid, dim3(256), 0, st, (const int64_t*)in, n, d, (int64_t*)Z, ldz);
-    else if (!z64 && !in64)
-        hipLaunchKernelGGL((to_coord_major_kernel<int32_t, int32_t>), grid, dim3(256), 0, st, (const int32_t*)in, n, d, (int32_t*)Z, ldz);
-    else
-        return hipErrorInvalidValue;
+    LGS_ZT(zb, ZT, LGS_ZT(ib, IT, hipLaunchKernelGGL((to_coord_major_kernel<ZT, IT>), grid, dim3(256), 0, st, (const IT*)in, n, d, (ZT*)Z, ldz)));
     return hipGetLastError();
 }
 
-hipError_t bz(const void* Z, bool z64, int64_t ldz, const double* BT, int d, int64_t n, double* V,
+hipError_t bz(const void* Z, int zb, int64_t ldz, const double* BT, int d, int64_t n, double* V,
               int64_t ldv, int64_t rb, int64_t rstride, int64_t roff, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
-    if (z64)
-        hipLaunchKernelGGL(bz_gemm_kernel<int64_t>, grid, dim3(256), 0, st, (const int64_t*)Z, ldz, BT, d, n, V, ldv, rb, rstride, roff);
-    else
-        hipLaunchKernelGGL(bz_gemm_kernel<int32_t>, grid, dim3(256), 0, st, (const int32_t*)Z, ldz, BT, d, n, V, ldv, rb, rstride, roff);
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_gemm_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, BT, d, n, V, ldv, rb, rstride, roff));
     return hipGetLastError();
 }
 
-hipError_t bz_i8(const void* Z, bool z64, int64_t ldz, const int8_t* Bd1, const int8_t* Bd0, int dc,
+hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int8_t* Bd1, const int8_t* Bd0, int dc,
                  int d, int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((d + 127) / 128), (unsigned)((n + 63) / 64));
-    if (z64)
-        hipLaunchKernelGGL(bz_i8_kernel<int64_t>, grid, dim3(256), 0, st, (const int64_t*)Z, ldz, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags);
-    else
-        hipLaunchKernelGGL(bz_i8_kernel<int32_t>, grid, dim3(256), 0, st, (const int32_t*)Z, ldz, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags);
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags));
     return hipGetLastError();
 }
 
