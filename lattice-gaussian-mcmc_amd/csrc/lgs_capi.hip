@@ -14,6 +14,7 @@
 
 #include "../../include/lgs.h"
 #include "lgs_kernels.h"
+#include "lgs_szc_host.h"
 
 namespace {
 
@@ -93,6 +94,9 @@ struct lgs_ctx {
     bool has_B = false;
     DevBuf R, RP, RC, BT, coord;  // coord: cp | rii | sig | sig_ref | lterm | irii | ros | isr
     DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
+    DevBuf etab;                  // SampleZ erf/exp table (lgs_device.h erf_gauss)
+    DevBuf szc;                   // per-coordinate SampleZ constants (lgs_kernels.h kSzc*)
+    bool libm_samplez = false;    // LGS_SAMPLEZ_LIBM=1: ocml erf/exp/erfinv path instead
     bool has_Bi8 = false;
     int64_t bd_rows = 0, bd_cols = 0;
     std::vector<BzCall> pending_i8;
@@ -220,6 +224,8 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
     a.sigma = c->sigma;
     a.seed = seed;
     a.flags = c->flags.as<unsigned int>();
+    a.etab = c->libm_samplez ? nullptr : c->etab.as<double>();
+    a.szc = c->libm_samplez ? nullptr : c->szc.as<double>();
     return a;
 }
 
@@ -317,6 +323,26 @@ int lgs_create(lgs_ctx** out, int device) {
         long long v = atoll(m);
         if (v >= 64) c->max_props = v;
     }
+    if (const char* m = getenv("LGS_SAMPLEZ_LIBM")) c->libm_samplez = atoi(m) != 0;
+    {
+        // {erf(j/64), exp(-(j/64)^2)}, j = 0..kErfTabLast, rounded from long double.
+        std::vector<double> tab(2 * (lgs::kErfTabLast + 1));
+        for (int j = 0; j <= lgs::kErfTabLast; ++j) {
+            const long double y = (long double)j / 64.0L;
+            tab[2 * j] = (double)erfl(y);
+            tab[2 * j + 1] = (double)expl(-y * y);
+        }
+        int rc = c->etab.reserve(tab.size() * 8);
+        if (!rc) {
+            e = hipMemcpy(c->etab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice);
+            if (e != hipSuccess) rc = fail(LGS_ERR_HIP, "etab upload: %s", hipGetErrorString(e));
+        }
+        if (rc) {
+            (void)hipStreamDestroy(c->own);
+            delete c;
+            return rc;
+        }
+    }
     *out = c;
     return LGS_OK;
 }
@@ -341,6 +367,7 @@ int lgs_set_stream(lgs_ctx* c, void* s) {
     c->stream = s ? (hipStream_t)s : c->own;
     return LGS_OK;
 }
+
 
 int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, const double* B,
                   double sigma, int32_t precision, uint32_t flags) {
@@ -374,6 +401,14 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
         co[6 * dd + i] = rii / sigma;
         co[7 * dd + i] = 1.0 / sref;
     }
+    std::vector<double> szc(dd * lgs::kSzcStride);
+    for (size_t i = 0; i < dd; ++i) lgs_host::build_szc(co[2 * dd + i], precision, szc.data() + i * lgs::kSzcStride);
+    if (getenv("LGS_DEBUG_SZC")) {
+        int hist[5] = {0, 0, 0, 0, 0};
+        for (size_t i = 0; i < dd; ++i) hist[(int)szc[i * lgs::kSzcStride + 2]]++;
+        fprintf(stderr, "lgs: SampleZ kinds round %d small %d closed %d capped %d generic %d\n", hist[0],
+                hist[1], hist[2], hist[3], hist[4]);
+    }
     // panel layouts (lgs_kernels.hip, klein_panel_kernel)
     const int64_t npan = (d + PB - 1) / PB;
     size_t rp_elems = (size_t)PB * PB * (size_t)(npan * (npan - 1) / 2);
@@ -397,8 +432,10 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
         }
     }
     if ((rc = c->R.reserve(dd * dd * 8)) || (rc = c->RP.reserve(rp.size() * 8)) ||
-        (rc = c->RC.reserve(rcv.size() * 8)) || (rc = c->coord.reserve(co.size() * 8)))
+        (rc = c->RC.reserve(rcv.size() * 8)) || (rc = c->coord.reserve(co.size() * 8)) ||
+        (rc = c->szc.reserve(szc.size() * 8)))
         return rc;
+    HIP_TRY(hipMemcpy(c->szc.p, szc.data(), szc.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->R.p, R, dd * dd * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->RP.p, rp.data(), rp.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->RC.p, rcv.data(), rcv.size() * 8, hipMemcpyHostToDevice));
@@ -792,7 +829,12 @@ int lgs_sample_z(lgs_ctx* c, int64_t n, const double* mu, const double* sigma, c
     HIP_TRY(hipMemcpyAsync(du, u, n * 8, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(lgs::launch::samplez_probe(dmu, dsig, du, n, precision,
                                        (flags & LGS_BASIS_LINEAR_PROBS) ? 1 : 0,
-                                       (flags & LGS_SAMPLEZ_TABLE) ? 1 : 0, dz, dln, c->stream));
+                                       (flags & LGS_SAMPLEZ_TABLE)      ? 1
+                                       : (flags & LGS_SAMPLEZ_DECISION) ? 2
+                                                                        : 0,
+                                       (c->libm_samplez || (flags & LGS_SAMPLEZ_LIBM)) ? nullptr
+                                                                      : c->etab.as<double>(),
+                                       dz, dln, c->stream));
     HIP_TRY(hipMemcpyAsync(z_out, dz, n * 8, hipMemcpyDeviceToHost, c->stream));
     if (log_norm_out)
         HIP_TRY(hipMemcpyAsync(log_norm_out, dln, n * 8, hipMemcpyDeviceToHost, c->stream));

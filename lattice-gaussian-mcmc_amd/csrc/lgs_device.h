@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "lgs_kernels.h"
+
 namespace lgs {
 
 constexpr uint32_t kTagCoord = 0;
@@ -187,6 +189,142 @@ __device__ __noinline__ double em_P(double x, double mu, double sig, double is, 
     return fma(-em_H(t, is), fx, sig * kSqrtHalfPi * erf(t * kInvSqrt2));
 }
 
+// Branch-free erf / Gaussian for the Euler-Maclaurin path.  etab holds, for
+// y_j = j/64 (j = 0..kErfTabLast = 512), the correctly rounded pair {erf(y_j),
+// exp(-y_j^2)} (filled on the host in long double, lgs_create).  With
+// h = y - y_j, |h| <= 1/128:
+//   erf(y)    = erf(y_j) + 2/sqrt(pi) e^{-y_j^2} sum_{n=1..7} (-1)^{n-1} H_{n-1}(y_j) h^n/n!
+//   e^{-y^2}  = e^{-y_j^2} exp(-(2 y_j h + h^2)),  |2 y_j h + h^2| <= 0.26,
+// (H_n physicists' Hermite polynomials; truncation < 1e-19 and < 1e-17 relative),
+// so both cost a 16-byte table load and ~30 FMAs, with no data-dependent
+// branches (ocml's erf selects one of several polynomials per lane).
+// |y| > 8 returns (sign 1, 0): erfc(8) = 1e-29 and e^{-64} = 2e-28 are far below
+// the fp64 resolution of S >= 10 (sigma >= 4).  The table (8.2 KB) is read from
+// LDS in the Klein kernels (TP = lds pointer) and from global memory elsewhere.
+using lds_cdptr = const __attribute__((address_space(3))) double*;
+
+struct ErfExp {
+    double erf, g;  // erf(y), exp(-y^2)
+};
+
+template <typename TP>
+__device__ __forceinline__ ErfExp erf_gauss(double y, TP etab) {
+    const double ay = fmin(fabs(y), 8.0);
+    const double jd = rint(ay * 64.0);
+    const int j = (int)jd;
+    const double y0 = jd * (1.0 / 64.0);
+    const double h = ay - y0;
+    const double F = etab[2 * j], G = etab[2 * j + 1];
+    const double y2 = y0 + y0;
+    const double H1 = y2;
+    const double H2 = fma(y2, H1, -2.0);
+    const double H3 = fma(y2, H2, -4.0 * H1);
+    const double H4 = fma(y2, H3, -6.0 * H2);
+    const double H5 = fma(y2, H4, -8.0 * H3);
+    const double H6 = fma(y2, H5, -10.0 * H4);
+    double q = fma(-h * (1.0 / 7.0), H6, H5);
+    q = fma(-h * (1.0 / 6.0), q, H4);
+    q = fma(-h * (1.0 / 5.0), q, H3);
+    q = fma(-h * (1.0 / 4.0), q, H2);
+    q = fma(-h * (1.0 / 3.0), q, H1);
+    q = fma(-h * 0.5, q, 1.0);
+    const double e = fma(1.1283791670955126 * G, h * q, F);  // 2/sqrt(pi)
+    // exp(-x), x = 2 y0 h + h^2 in [-0.26, 0.26]: degree-12 Taylor
+    const double x = -fma(y2, h, h * h);
+    double p = fma(x, 1.0 / 479001600.0, 1.0 / 39916800.0);
+    p = fma(x, p, 1.0 / 3628800.0);
+    p = fma(x, p, 1.0 / 362880.0);
+    p = fma(x, p, 1.0 / 40320.0);
+    p = fma(x, p, 1.0 / 5040.0);
+    p = fma(x, p, 1.0 / 720.0);
+    p = fma(x, p, 1.0 / 120.0);
+    p = fma(x, p, 1.0 / 24.0);
+    p = fma(x, p, 1.0 / 6.0);
+    p = fma(x, p, 0.5);
+    p = fma(x, p, 1.0);
+    p = fma(x, p, 1.0);
+    const bool big = fabs(y) > 8.0;
+    ErfExp r;
+    r.erf = copysign(big ? 1.0 : e, y);
+    r.g = big ? 0.0 : G * p;
+    return r;
+}
+
+// P(x) of the Euler-Maclaurin formula with NT Hermite correction terms
+// (NT = 6 for sigma < 50; 3 suffice above: the next term is < 1e-18 S).
+#define LGS_EM_ATTR __device__ __forceinline__
+template <int NT, typename TP>
+LGS_EM_ATTR double em_P_tab(double x, double mu, double sig, double is, TP etab, double& fx) {
+    const double t = (x - mu) * is;
+    const ErfExp ee = erf_gauss(t * kInvSqrt2, etab);
+    fx = ee.g;
+    const double c[6] = {1.0 / 12.0, -1.0 / 720.0, 1.0 / 30240.0, -1.0 / 1209600.0,
+                         1.0 / 47900160.0, -5.284190138687493e-10};
+    const double is2 = is * is;
+    double hm = 1.0, h = t, p = is, res = 0.0, n = 1.0;
+#pragma unroll
+    for (int m = 0; m < NT; ++m) {
+        res = fma(c[m] * p, h, res);
+        if (m + 1 < NT) {
+            double h2 = fma(t, h, -n * hm);
+            n += 1.0;
+            hm = h;
+            h = h2;
+            h2 = fma(t, h, -n * hm);
+            n += 1.0;
+            hm = h;
+            h = h2;
+            p *= is2;
+        }
+    }
+    return fma(-res, fx, sig * kSqrtHalfPi * ee.erf);
+}
+
+template <typename TP>
+LGS_EM_ATTR double gauss_tab(double kd, double mu, double is, TP etab) {
+    return erf_gauss((kd - mu) * is * kInvSqrt2, etab).g;
+}
+
+// Euler-Maclaurin decision with the tabulated erf/exp.  The initial guess uses
+// fp32 erfinvf (its error is absorbed by the +-1 steps); the decision rule,
+// margins and table fallback are those of the libm path below.
+template <int NT, typename TP>
+__device__ __forceinline__ SampleZOut sample_z_em_tab(double mu, double sig, int precision,
+                                                      bool linear_probs, double u, bool want_log,
+                                                      int64_t lo, int64_t hi, TP etab) {
+    const double is = 1.0 / sig;
+    double fL, fU, fk;
+    const double PL = em_P_tab<NT>((double)lo, mu, sig, is, etab, fL);
+    const double PU = em_P_tab<NT>((double)hi, mu, sig, is, etab, fU);
+    const double S = (PU - PL) + 0.5 * (fL + fU);
+    const double target = u * S;
+    const double base = PL - 0.5 * fL;
+    const float arg = fminf(fmaxf((float)((target + base) / (sig * kSqrtHalfPi)), -1.0f + 0x1p-24f),
+                            1.0f - 0x1p-24f);
+    const double x = mu + sig * kSqrt2 * (double)erfinvf(arg);
+    double kd = fmin(fmax(ceil(x - 0.5), (double)lo), (double)hi);
+    double Ck = em_P_tab<NT>(kd, mu, sig, is, etab, fk) + 0.5 * fk - base;
+    const double fhi = (double)hi, flo = (double)lo;
+    for (int it = 0; it < 64 && Ck <= target && kd < fhi; ++it) {  // move up
+        kd += 1.0;
+        fk = gauss_tab(kd, mu, is, etab);
+        Ck += fk;
+    }
+    for (int it = 0; it < 64 && kd > flo && Ck - fk > target; ++it) {  // move down
+        Ck -= fk;
+        kd -= 1.0;
+        fk = gauss_tab(kd, mu, is, etab);
+    }
+    const double margin = fmin(Ck - target, kd > flo ? target - (Ck - fk) : target);
+    if (!(margin > 1e-12 * S) || !(Ck > target)) {
+        return sample_z_table(mu, sig, precision, linear_probs, u, want_log);
+    }
+    SampleZOut out;
+    out.z = (int64_t)kd;
+    out.log_norm = want_log ? log(S) : 0.0;
+    return out;
+}
+
 // Not inlined: inlining lets the compiler hoist the ~100 polynomial constants of
 // erf/erfinv/exp/log out of the coordinate loop into registers (measured: 398
 // VGPR+AGPR, 1 wave/SIMD); as a call the kernel stays at <= 170 VGPRs.
@@ -246,8 +384,9 @@ __device__ __forceinline__ bool sample_z_small(double mu, double sig, int precis
     return true;
 }
 
+// etab == nullptr selects the libm Euler-Maclaurin path (ocml erf/exp/erfinv).
 LGS_SAMPLEZ_ATTR SampleZOut sample_z(double mu, double sig, int precision, bool linear_probs,
-                                     double u, bool want_log = true) {
+                                     double u, bool want_log, const double* __restrict__ etab) {
     if (sig < kEMMin) {
         SampleZOut o;
         if (sample_z_small(mu, sig, precision, linear_probs, u, want_log, o)) return o;
@@ -255,6 +394,10 @@ LGS_SAMPLEZ_ATTR SampleZOut sample_z(double mu, double sig, int precision, bool 
     }
     int64_t lo, hi;
     support_window(mu, sig, precision, lo, hi);
+    if (etab) {
+        return sig < 50.0 ? sample_z_em_tab<6>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab)
+                          : sample_z_em_tab<3>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab);
+    }
     const double is = 1.0 / sig;
     double fL, fU, fk;
     const double PL = em_P((double)lo, mu, sig, is, fL);
@@ -289,6 +432,147 @@ LGS_SAMPLEZ_ATTR SampleZOut sample_z(double mu, double sig, int precision, bool 
     out.z = (int64_t)kd;
     out.log_norm = want_log ? log(S) : 0.0;
     return out;
+}
+
+// ------------------------------------------------- SampleZ on the Klein path
+// Same decisions as sample_z, using the per-coordinate constants q (layout:
+// lgs_kernels.h kSzc*): no divisions, no 64-bit integer arithmetic, and for
+// the wide windows the two window-end evaluations of S and base are replaced by
+// the closed form (uncapped, rf >= 9: the tails beyond +-9 sigma are < 1e-18 S)
+// or by host-fitted polynomials in m = mu - rint(mu) (capped windows; fitted
+// and checked to 4e-17 S in long double, lgs_capi.hip build_szc).  Returns z as
+// an exact fp64 integer.
+template <int NT, typename TP>
+__device__ __forceinline__ double em_C_rel(double kd, double m, double sig, double is, TP etab,
+                                           double base, double& fk) {
+    // C(k) = P(k) + f(k)/2 - base with k - mu = kd - m (exact to one rounding)
+    return em_P_tab<NT>(kd, m, sig, is, etab, fk) + 0.5 * fk - base;
+}
+
+template <int NT, typename TP>
+__device__ __forceinline__ double sample_z_wide(double mu, double u, const double* __restrict__ q,
+                                                int kind, int precision, bool linear_probs,
+                                                bool want_log, TP etab, double& log_norm) {
+    const double sig = q[0], is = q[1];
+    const double c = rint(mu);
+    const double m = mu - c;
+    double S, base, a, b;
+    if (kind == kSzCapped) {
+        S = q[9 + kSzDeg];
+        base = q[20 + kSzDeg];
+#pragma unroll
+        for (int k = kSzDeg - 1; k >= 0; --k) {
+            S = fma(S, m, q[9 + k]);
+            base = fma(base, m, q[20 + k]);
+        }
+        a = -500.0;
+        b = 500.0;
+    } else {
+        S = q[7];
+        base = q[8];
+        a = floor(mu - q[6]) - c;
+        b = ceil(mu + q[6]) - c;
+    }
+    const double target = u * S;
+    const float arg = fminf(fmaxf((float)((target + base) * q[4]), -1.0f + 0x1p-24f),
+                            1.0f - 0x1p-24f);
+    const float xg = fmaf((float)q[5], erfinvf(arg), (float)m);
+    double kd = fmin(fmax((double)ceilf(xg - 0.5f), a), b);
+    double fk;
+    double Ck = em_C_rel<NT>(kd, m, sig, is, etab, base, fk);
+    for (int it = 0; it < 64 && Ck <= target && kd < b; ++it) {  // move up
+        kd += 1.0;
+        fk = gauss_tab(kd, m, is, etab);
+        Ck += fk;
+    }
+    for (int it = 0; it < 64 && kd > a && Ck - fk > target; ++it) {  // move down
+        Ck -= fk;
+        kd -= 1.0;
+        fk = gauss_tab(kd, m, is, etab);
+    }
+    const double margin = fmin(Ck - target, kd > a ? target - (Ck - fk) : target);
+    if (!(margin > 1e-12 * S) || !(Ck > target)) {
+        const SampleZOut o = sample_z_table(mu, sig, precision, linear_probs, u, want_log);
+        log_norm = o.log_norm;
+        return (double)o.z;
+    }
+    log_norm = want_log ? log(S) : 0.0;
+    return c + kd;
+}
+
+// A wave-uniform pointer passed to a non-inlined function arrives in VGPRs;
+// readfirstlane makes it scalar so its loads are s_load into SGPRs.
+template <typename T>
+__device__ __forceinline__ const T* uniform_ptr(const T* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const T*)(((uint64_t)hi << 32) | lo);
+}
+
+template <typename TP>
+LGS_SAMPLEZ_ATTR double sample_z_coord(double mu, double u, const double* __restrict__ qv,
+                                       int precision, bool linear_probs, bool want_log, TP etab,
+                                       double& log_norm) {
+    const double* __restrict__ q = uniform_ptr(qv);  // all lanes are on the same coordinate
+    const int kind = (int)q[2];
+    const double sig = q[0];
+    if (kind == kSzSmall) {
+        const double lo = floor(mu - q[6]);
+        const double hi = ceil(mu + q[6]);
+        if (hi - lo > 3.0) {
+            const SampleZOut o = sample_z_table(mu, sig, precision, linear_probs, u, want_log);
+            log_norm = o.log_norm;
+            return (double)o.z;
+        }
+        const double is = q[1];
+        double e[4];
+        double emax = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double t = ((lo + (double)k) - mu) * is;
+            e[k] = lo + (double)k <= hi ? -0.5 * (t * t) : -INFINITY;
+            emax = fmax(emax, e[k]);
+        }
+        if (linear_probs && emax < -745.2) {
+            log_norm = -INFINITY;
+            return rint(mu);
+        }
+        double w[4];
+        double Ssum = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const double x = e[k] - emax;
+            w[k] = x == 0.0 ? 1.0 : (x < -745.2 ? 0.0 : exp(x));
+            Ssum += w[k];
+        }
+        const double target = u * Ssum;
+        double C = 0.0, z = hi;
+        bool found = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            C += w[k];
+            if (!found && lo + (double)k <= hi && C > target) {
+                z = lo + (double)k;
+                found = true;
+            }
+        }
+        log_norm = want_log ? emax + log(Ssum) : 0.0;
+        return z;
+    }
+    if (kind == kSzGeneric) {
+        int64_t lo, hi;
+        support_window(mu, sig, precision, lo, hi);
+        const SampleZOut o =
+            sig < 50.0
+                ? sample_z_em_tab<6>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab)
+                : sample_z_em_tab<3>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab);
+        log_norm = o.log_norm;
+        return (double)o.z;
+    }
+    return sig < 50.0
+               ? sample_z_wide<6>(mu, u, q, kind, precision, linear_probs, want_log, etab, log_norm)
+               : sample_z_wide<3>(mu, u, q, kind, precision, linear_probs, want_log, etab, log_norm);
 }
 
 }  // namespace lgs

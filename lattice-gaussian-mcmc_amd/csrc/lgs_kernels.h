@@ -11,6 +11,23 @@ constexpr unsigned int kFlagOverflow = 2u;   // |z| >= 2^31 with an int32 store
 constexpr unsigned int kFlagI8Range = 4u;    // |z| > 32639: int8-digit B z must be redone in fp64
 constexpr unsigned int kFlagOverflow16 = 8u; // |z| > 32767 in a 16-bit internal store
 
+constexpr int kErfTabLast = 512;  // SampleZ erf/exp table: y_j = j/64, j = 0..kErfTabLast (y <= 8)
+
+// Per-coordinate SampleZ constants (kSzcStride doubles per coordinate, built by
+// the host in lgs_set_basis; lgs_device.h sample_z_coord):
+//   [0] sigma_i  [1] 1/sigma_i  [2] kind  [3] sc = sigma*sqrt(pi/2)  [4] 1/sc
+//   [5] sigma*sqrt(2)  [6] rf*sigma (window half-width, klein.py:113-120)
+//   [7] S, [8] base (kind kSzClosed)
+//   [9..9+kSzDeg] / [20..20+kSzDeg]: monomial coefficients in m = mu - rint(mu)
+//   of S(m) / base(m) (kind kSzCapped)
+constexpr int kSzcStride = 32;
+constexpr int kSzDeg = 10;
+constexpr int kSzRound = 0;    // sigma_i < 1e-10: round(mu), no draw
+constexpr int kSzSmall = 1;    // sigma_i < 4: <= 4-point exponent path / table walk
+constexpr int kSzClosed = 2;   // uncapped window of +-rf*sigma, rf >= 9: S = 2 sc, base = -sc
+constexpr int kSzCapped = 3;   // window capped to rint(mu) +- 500: S(m), base(m) polynomials
+constexpr int kSzGeneric = 4;  // anything else: both window ends evaluated per draw
+
 constexpr int kKernelExact = 0;  // reference-order back-substitution
 constexpr int kKernelValu = 1;   // blocked panel kernel, VALU far field
 constexpr int kKernelMfma = 2;   // blocked panel kernel, fp64 MFMA far field
@@ -47,6 +64,8 @@ struct KleinArgs {
     int64_t ldz;
     double* LW;
     unsigned int* flags;
+    const double* etab;  // SampleZ erf/exp table (nullptr: ocml libm path)
+    const double* szc;   // per-coordinate SampleZ constants (nullptr: generic sample_z)
 };
 
 struct AcceptArgs {
@@ -72,7 +91,7 @@ hipError_t klein(const KleinArgs& a, const double* R, const double* RP, const do
                  int panel, int kernel, bool wl, int zb, void* Z, hipStream_t st);
 hipError_t accept(const AcceptArgs& a, hipStream_t st);
 hipError_t samplez_probe(const double* mu, const double* sig, const double* u, int64_t n,
-                         int precision, int linear, int force_table, int64_t* z, double* ln,
+                         int precision, int linear, int mode, const double* etab, int64_t* z, double* ln,
                          hipStream_t st);
 hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, int zb, double* out,
                        hipStream_t st);

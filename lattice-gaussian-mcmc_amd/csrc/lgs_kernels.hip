@@ -37,33 +37,38 @@ __device__ __forceinline__ void lane_counter(const KleinArgs& a, int64_t p, uint
 }
 
 // One coordinate's decision + weight bookkeeping, shared by both samplers.
-template <bool WL>
-__device__ __forceinline__ int64_t decide_coord(const KleinArgs& a, int i, double mu,
-                                                CoordStream& rs, double& lw,
-                                                unsigned int& flags) {
-    const double s = a.sig[i];
-    int64_t zi;
+template <bool WL, typename TP>
+__device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double mu,
+                                               CoordStream& rs, double& lw, unsigned int& flags,
+                                               TP etab) {
+    double zi;
     if (!isfinite(mu)) {
         flags |= kFlagNonFinite;
-        return 0;
+        return 0.0;
     }
+    const double s = a.szc ? a.szc[(size_t)i * kSzcStride] : a.sig[i];
 #ifdef LGS_DIAG_NO_SAMPLEZ
     if (true) {  // diagnostic build: SampleZ replaced by rounding
-        zi = (int64_t)rint(mu + rs.u((uint32_t)(a.d - 1 - i)) * 1e-300);
+        zi = rint(mu + rs.u((uint32_t)(a.d - 1 - i)) * 1e-300);
     } else
 #endif
     if (s == 0.0) {  // sigma_i < 1e-10: round, no draw (klein.py:201-204)
-        zi = (int64_t)rint(mu);
+        zi = rint(mu);
+    } else if (a.szc) {
+        double ln;
+        zi = sample_z_coord(mu, rs.u((uint32_t)(a.d - 1 - i)), a.szc + (size_t)i * kSzcStride,
+                            a.precision, a.linear_probs != 0, WL, etab, ln);
+        if (WL) lw += ln;
     } else {
         SampleZOut o = sample_z(mu, s, a.precision, a.linear_probs != 0,
-                                rs.u((uint32_t)(a.d - 1 - i)), WL);
-        zi = o.z;
+                                rs.u((uint32_t)(a.d - 1 - i)), WL, a.etab);
+        zi = (double)o.z;
         if (WL) lw += o.log_norm;
     }
     if (!WL) {
         // Reference-mode importance weight (imhk.py:102-124): log_gaussian_weight(Bz)
         // - compute_log_density(Bz), with ||Bz - c||^2 = sum_i (R_ii (z_i - mu_i))^2.
-        const double res = (double)zi - mu;
+        const double res = zi - mu;
         const double ta = res * a.ros[i];
         const double tq = res * a.isr[i];
         lw += (-0.5 * (ta * ta)) - (-0.5 * (tq * tq) - a.lterm[i]);
@@ -71,11 +76,25 @@ __device__ __forceinline__ int64_t decide_coord(const KleinArgs& a, int i, doubl
     return zi;
 }
 
+// z is an exact fp64 integer; int64 stores convert it, narrower stores flag
+// values outside their range.
 template <typename ZT>
-__device__ __forceinline__ void store_z(ZT* Z, size_t off, int64_t zi, unsigned int& flags) {
-    if (sizeof(ZT) == 4 && (zi > 2147483647LL || zi < -2147483648LL)) flags |= kFlagOverflow;
-    if (sizeof(ZT) == 2 && (zi > 32767 || zi < -32768)) flags |= kFlagOverflow16;
-    Z[off] = (ZT)zi;
+__device__ __forceinline__ void store_z(ZT* Z, size_t off, double zi, unsigned int& flags) {
+    if (sizeof(ZT) == 8) {
+        Z[off] = (ZT)(int64_t)zi;
+        return;
+    }
+    if (sizeof(ZT) == 4 && !(zi <= 2147483647.0 && zi >= -2147483648.0)) flags |= kFlagOverflow;
+    if (sizeof(ZT) == 2 && !(zi <= 32767.0 && zi >= -32768.0)) flags |= kFlagOverflow16;
+    Z[off] = (ZT)(int)fmin(fmax(zi, -2147483648.0), 2147483647.0);
+}
+
+// Stages the SampleZ erf/exp table in LDS (block-wide; call before any early return).
+__device__ __forceinline__ lds_cdptr stage_etab(double* tab_lds, const double* __restrict__ etab) {
+    if (etab)
+        for (int k = threadIdx.x; k < 2 * (kErfTabLast + 1); k += blockDim.x) tab_lds[k] = etab[k];
+    __syncthreads();
+    return (lds_cdptr)tab_lds;
 }
 
 // ------------------------------------------------------------ exact order
@@ -83,6 +102,8 @@ template <typename ZT, bool WL>
 __global__ __launch_bounds__(256) void klein_exact_kernel(const KleinArgs a,
                                                           const double* __restrict__ R,
                                                           ZT* __restrict__ Z) {
+    __shared__ double tab_lds[2 * (kErfTabLast + 1)];
+    const lds_cdptr etab_s = stage_etab(tab_lds, a.etab);
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.n) return;
     uint32_t chain, step;
@@ -98,7 +119,7 @@ __global__ __launch_bounds__(256) void klein_exact_kernel(const KleinArgs a,
         double cs = 0.0;
         for (int j = i + 1; j < d; ++j) cs = cs + Ri[j] * (double)Z[(size_t)j * ldz + p];
         const double mu = (a.cp[i] - cs) / a.rii[i];
-        const int64_t zi = decide_coord<WL>(a, i, mu, rs, lw, flags);
+        const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s);
         store_z(Z, (size_t)i * ldz + p, zi, flags);
     }
     if (a.LW) a.LW[p] = lw;
@@ -116,6 +137,8 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
                                                           const double* __restrict__ RP,
                                                           const double* __restrict__ RC,
                                                           ZT* __restrict__ Z) {
+    __shared__ double tab_lds[2 * (kErfTabLast + 1)];
+    const lds_cdptr etab_s = stage_etab(tab_lds, a.etab);
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.n) return;
     uint32_t chain, step;
@@ -153,9 +176,9 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
         for (int s = 0; s < rows; ++s) {
             const int i = p_hi - 1 - s;
             const double mu = (a.cp[i] - acc[PB - 1]) * a.irii[i];
-            const int64_t zi = decide_coord<WL>(a, i, mu, rs, lw, flags);
+            const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s);
             store_z(Z, (size_t)i * ldz + p, zi, flags);
-            const double x = (double)zi;
+            const double x = zi;
             const double* __restrict__ rc = RC + (size_t)i * (PB - 1);
 #pragma unroll
             for (int k = 0; k < PB - 1; ++k) acc[k] = fma(rc[PB - 2 - k], x, acc[k]);
@@ -184,23 +207,36 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
 typedef int v4i32_t __attribute__((ext_vector_type(4)));
 typedef double d4_t __attribute__((ext_vector_type(4)));
 
+// Four consecutive coefficients of one coordinate row (one MFMA B fragment
+// column group), loaded non-temporally; raw storage per type, converted to fp64
+// when the MFMA consumes them (64-bit values are converted exactly).
 template <typename ZT>
-__device__ __forceinline__ v4i32_t load4_nt(const ZT* p) {
-    v4i32_t v;
-    if constexpr (sizeof(ZT) == 2) {
-        const unsigned long long w = __builtin_nontemporal_load((const unsigned long long*)p);
-        v[0] = (int)(short)(w & 0xffff);
-        v[1] = (int)(short)((w >> 16) & 0xffff);
-        v[2] = (int)(short)((w >> 32) & 0xffff);
-        v[3] = (int)(short)(w >> 48);
-    } else if constexpr (sizeof(ZT) == 4) {
-        v = __builtin_nontemporal_load((const v4i32_t*)p);
-    } else {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) v[g] = (int)__builtin_nontemporal_load(p + g);
+struct ZQuad;
+template <>
+struct ZQuad<int16_t> {
+    unsigned long long w;
+    __device__ __forceinline__ void load(const int16_t* p) {
+        w = __builtin_nontemporal_load((const unsigned long long*)p);
     }
-    return v;
-}
+    __device__ __forceinline__ double get(int g) const { return (double)(short)(w >> (16 * g)); }
+};
+template <>
+struct ZQuad<int32_t> {
+    v4i32_t v;
+    __device__ __forceinline__ void load(const int32_t* p) {
+        v = __builtin_nontemporal_load((const v4i32_t*)p);
+    }
+    __device__ __forceinline__ double get(int g) const { return (double)v[g]; }
+};
+template <>
+struct ZQuad<int64_t> {
+    long long v[4];
+    __device__ __forceinline__ void load(const int64_t* p) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) v[g] = __builtin_nontemporal_load((const long long*)p + g);
+    }
+    __device__ __forceinline__ double get(int g) const { return (double)v[g]; }
+};
 
 template <typename ZT, int PB, bool WL>
 #ifndef LGS_MFMA_LB32
@@ -212,6 +248,8 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
                                                             ZT* __restrict__ Z) {
     constexpr int NT = PB / 16, LDF = 65;  // LDS tile pitch (doubles): conflict-free row reads
     __shared__ double Fl[4][16 * LDF];
+    __shared__ double tab_lds[2 * (kErfTabLast + 1)];
+    const lds_cdptr etab_s = stage_etab(tab_lds, a.etab);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t p0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
     if (p0 >= a.n) return;  // whole waves only (n % 64 == 0)
@@ -245,38 +283,50 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
             for (int t = 0; t < NT; ++t)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) f[t][g] = (d4_t){0.0, 0.0, 0.0, 0.0};
-            const double* __restrict__ rp = RP + (size_t)PB * PB * ((size_t)pk * (pk - 1) / 2);
-            const ZT* zcol = Z + p0 + 4 * nq;
-            // software pipeline, 4 stages: the loads of step j0+16 are issued while
-            // the MFMAs of step j0 run (VMEM returns in order, so each wait is a
-            // counted vmcnt); K = d - p_hi is a multiple of 16
+            // Stage s of step j0 covers columns jj = j0 + 4s: lane (kq, nq) reads
+            // R rows 16t + nq at column jj + kq (RP panel block, PB doubles per
+            // column) and the 4 coefficients of chains 4nq..4nq+3 at coordinate
+            // jj + kq.  Uniform base pointers advance by one stage (4 columns);
+            // the per-lane offsets are fixed.  Software pipeline, 4 stages deep:
+            // the loads of step j0 + 16 are issued while the MFMAs of step j0
+            // run; K = d - p_hi is a multiple of PB, so every step is full.
+            const double* __restrict__ rbase = RP + (size_t)PB * PB * ((size_t)pk * (pk - 1) / 2);
+            const ZT* __restrict__ zbase = Z + p0 + (size_t)p_hi * ldz;
+            const size_t roff = (size_t)kq * PB + nq, zoff = (size_t)kq * ldz + 4 * nq;
+            const size_t rstep = 4 * PB, zstep = 4 * ldz;
             double ra[4][NT];
-            v4i32_t zb[4];
-            auto load_stage = [&](int jj, double (&av)[NT], v4i32_t& zv) {
+            ZQuad<ZT> zq[4];
 #pragma unroll
-                for (int t = 0; t < NT; ++t) av[t] = rp[(size_t)(jj - p_hi + kq) * PB + 16 * t + nq];
-                zv = load4_nt(zcol + (size_t)(jj + kq) * ldz);
+            for (int st = 0; st < 4; ++st) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) ra[st][t] = rbase[roff + 16 * t];
+                zq[st].load(zbase + zoff);
+                rbase += rstep;
+                zbase += zstep;
+            }
+            auto consume = [&](int st) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const double bz = zq[st].get(g);
+#pragma unroll
+                    for (int t = 0; t < NT; ++t)
+                        f[t][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(ra[st][t], bz, f[t][g], 0, 0, 0);
+                }
             };
-#pragma unroll
-            for (int st = 0; st < 4; ++st) load_stage(p_hi + 4 * st, ra[st], zb[st]);
-            for (int j0 = p_hi; j0 < d; j0 += 16) {
+            int j0 = p_hi;
+            for (; j0 + 16 < d; j0 += 16) {
 #pragma unroll
                 for (int st = 0; st < 4; ++st) {
-                    double a_cur[NT];
+                    consume(st);
 #pragma unroll
-                    for (int t = 0; t < NT; ++t) a_cur[t] = ra[st][t];
-                    const v4i32_t z_cur = zb[st];
-                    const int jn = j0 + 16 + 4 * st;
-                    if (jn < d) load_stage(jn, ra[st], zb[st]);
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const double bz = (double)z_cur[g];
-#pragma unroll
-                        for (int t = 0; t < NT; ++t)
-                            f[t][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[t], bz, f[t][g], 0, 0, 0);
-                    }
+                    for (int t = 0; t < NT; ++t) ra[st][t] = rbase[roff + 16 * t];
+                    zq[st].load(zbase + zoff);
+                    rbase += rstep;
+                    zbase += zstep;
                 }
             }
+#pragma unroll
+            for (int st = 0; st < 4; ++st) consume(st);
             // D -> LDS [row][chain] -> one chain per lane, one 16-row tile at a time
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
@@ -298,9 +348,9 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
         for (int s = 0; s < rows; ++s) {
             const int i = p_hi - 1 - s;
             const double mu = (a.cp[i] - acc[PB - 1]) * a.irii[i];
-            const int64_t zi = decide_coord<WL>(a, i, mu, rs, lw, flags);
+            const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s);
             store_z(Z, (size_t)i * ldz + p, zi, flags);
-            const double x = (double)zi;
+            const double x = zi;
             const double* __restrict__ rc = RC + (size_t)i * (PB - 1);
 #pragma unroll
             for (int k = 0; k < PB - 1; ++k) acc[k] = fma(rc[PB - 2 - k], x, acc[k]);
@@ -347,13 +397,15 @@ __global__ __launch_bounds__(256) void samplez_probe_kernel(const double* __rest
                                                             const double* __restrict__ sig,
                                                             const double* __restrict__ u,
                                                             int64_t n, int precision,
-                                                            int linear, int force_table,
+                                                            int linear, int mode, const double* __restrict__ etab,
                                                             int64_t* __restrict__ z,
                                                             double* __restrict__ ln) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
-    SampleZOut o = force_table ? sample_z_table(mu[p], sig[p], precision, linear != 0, u[p])
-                               : sample_z(mu[p], sig[p], precision, linear != 0, u[p]);
+    // mode 0: sample_z with log-normaliser; 1: table walk; 2: decision only.
+    const SampleZOut o = mode == 1 ? sample_z_table(mu[p], sig[p], precision, linear != 0, u[p])
+                                   : sample_z(mu[p], sig[p], precision, linear != 0, u[p],
+                                              mode == 0, etab);
     z[p] = o.z;
     if (ln) ln[p] = o.log_norm;
 }
@@ -806,11 +858,11 @@ hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, int z
 }
 
 hipError_t samplez_probe(const double* mu, const double* sig, const double* u, int64_t n,
-                         int precision, int linear, int force_table, int64_t* z, double* ln,
+                         int precision, int linear, int mode, const double* etab, int64_t* z, double* ln,
                          hipStream_t st) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(samplez_probe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                       mu, sig, u, n, precision, linear, force_table, z, ln);
+                       mu, sig, u, n, precision, linear, mode, etab, z, ln);
     return hipGetLastError();
 }
 

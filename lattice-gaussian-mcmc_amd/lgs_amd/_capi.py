@@ -29,6 +29,8 @@ LGS_WANG_LING = 0x4
 LGS_Z64 = 0x8
 LGS_COORD_MAJOR = 0x10
 LGS_SAMPLEZ_TABLE = 0x20
+LGS_SAMPLEZ_DECISION = 0x40
+LGS_SAMPLEZ_LIBM = 0x80
 
 KERNEL_KLEIN, KERNEL_BZ, KERNEL_ACCEPT, KERNEL_MOMENTS = 0, 1, 2, 3
 
@@ -206,13 +208,15 @@ class Context:
                                     LGS_Z64 if z64 else 0))
         return out
 
-    def sample_z(self, mu, sigma, u, precision=10, table=False, linear_probs=False):
+    def sample_z(self, mu, sigma, u, precision=10, table=False, linear_probs=False, mode=None):
         mu = np.ascontiguousarray(mu, dtype=np.float64)
         sg = np.ascontiguousarray(np.broadcast_to(sigma, mu.shape), dtype=np.float64)
         uu = np.ascontiguousarray(u, dtype=np.float64)
         z = np.empty(mu.shape, dtype=np.int64)
         ln = np.empty(mu.shape)
         f = (LGS_SAMPLEZ_TABLE if table else 0) | (LGS_BASIS_LINEAR_PROBS if linear_probs else 0)
+        f |= {None: 0, "decision": LGS_SAMPLEZ_DECISION, "libm": LGS_SAMPLEZ_LIBM,
+              "libm_decision": LGS_SAMPLEZ_LIBM | LGS_SAMPLEZ_DECISION}[mode]
         _check(_lib.lgs_sample_z(self._h, mu.size, _ptr(mu), _ptr(sg), _ptr(uu), int(precision),
                                  _ptr(z), _ptr(ln), f))
         return z, ln

@@ -67,6 +67,47 @@ def test_klein_matches_oracle_seeded(ctx, oracle, case, mode):
         np.testing.assert_allclose(r["v"], o["v"], rtol=1e-12, atol=1e-9)
 
 
+@pytest.fixture(scope="module")
+def ctx_libm(capi):
+    """A context on the generic SampleZ path (ocml erf/exp/erfinv, no per-coordinate constants)."""
+    os.environ["LGS_SAMPLEZ_LIBM"] = "1"
+    try:
+        return capi.Context(0)
+    finally:
+        del os.environ["LGS_SAMPLEZ_LIBM"]
+
+
+def _wide_sigma_basis(d, seed):
+    """Upper-triangular basis whose sigma_i = sigma/R_ii span every SampleZ kind:
+    tiny (< 0.1), small (< 4), uncapped wide (4..50), capped (> 50), clamped (> 1e10)."""
+    rng = np.random.default_rng(seed)
+    sig_i = np.exp(rng.uniform(np.log(1e-3), np.log(3e3), d))
+    sig_i[::7] = rng.uniform(45, 55, len(sig_i[::7]))  # around the cap threshold
+    sig_i[3] = 1e11
+    diag = 10.0 / sig_i
+    R = np.diag(diag)
+    R[np.arange(d - 1), np.arange(1, d)] = diag[:-1] * rng.uniform(-0.5, 0.5, d - 1)
+    R[np.arange(d - 2), np.arange(2, d)] = diag[:-2] * rng.uniform(-0.2, 0.2, d - 2)
+    return R, rng.normal(size=d) * diag * 300.0
+
+
+@pytest.mark.parametrize("precision", [3, 8, 10, 20])
+@pytest.mark.parametrize("wl", [False, True])
+def test_klein_coord_constants_vs_generic_samplez(ctx, ctx_libm, oracle, capi, precision, wl):
+    """Per-coordinate SampleZ constants (closed-form / fitted window normalisers)
+    give the generic path's decisions and log-weights, and the oracle's z."""
+    R, cp = _wide_sigma_basis(96, precision)
+    out = []
+    flags = capi.LGS_WANG_LING if wl else 0
+    for c in (ctx, ctx_libm):
+        c.set_basis(R, cp, None, 10.0, precision=precision)
+        out.append(c.klein_host(99, 5, 3000, want_z=True, want_v=False, want_logw=True, flags=flags))
+    assert np.array_equal(out[0]["z"], out[1]["z"])
+    np.testing.assert_allclose(out[0]["logw"], out[1]["logw"], rtol=1e-12, atol=1e-9)
+    o = oracle.klein(R, cp, 10.0, 200, seed=99, first_sample=5, precision=precision)
+    assert np.array_equal(out[0]["z"][:200], o["z"])
+
+
 def test_klein_full_size_ntru1024_vs_oracle(ctx, oracle):
     """BASELINE config C3 basis (d = 1024): device vs oracle on 64 samples, both kernels."""
     from lgs_amd.lattices import build_config
@@ -278,6 +319,64 @@ def test_samplez_reference_decision_table(ctx, table):
     g = load_golden("samplez_table.npz")
     z, ln = ctx.sample_z(g["mu"], g["sigma"], g["u"], table=table)
     assert np.array_equal(z, g["z"])
+
+
+def _window(mu, sig, precision=10):
+    rf = np.where(sig < 0.1, max(precision, 3), precision).astype(np.float64)
+    lo = np.floor(mu - rf * sig).astype(np.int64)
+    hi = np.ceil(mu + rf * sig).astype(np.int64)
+    cap = hi - lo > 1000
+    c = np.rint(mu).astype(np.int64)
+    return np.where(cap, c - 500, lo), np.where(cap, c + 500, hi)
+
+
+def test_samplez_decision_golden(ctx):
+    """Decision-only mode (fp32 certificate for wide windows) on the reference's decisions."""
+    g = load_golden("samplez_table.npz")
+    z, _ = ctx.sample_z(g["mu"], g["sigma"], g["u"], mode="decision")
+    assert np.array_equal(z, g["z"])
+
+
+def test_samplez_near_boundaries(ctx):
+    """u placed at +-eps around exact CDF boundaries (long-double table sums):
+    the tabulated Euler-Maclaurin path, the libm path and the table walk agree
+    (draws inside the 1e-12 S margin go to the table walk in both EM paths)."""
+    rng = np.random.default_rng(77)
+    mus, sigs, us = [], [], []
+    for _ in range(300):
+        sig = float(np.exp(rng.uniform(np.log(4.0), np.log(1e6))))
+        mu = float(rng.uniform(-1, 1) * rng.choice([1.0, 50.0, 1e5]))
+        lo, hi = _window(np.array([mu]), np.array([sig]))
+        k = np.arange(lo[0], hi[0] + 1, dtype=np.longdouble)
+        w = np.exp(-0.5 * ((k - np.longdouble(mu)) / np.longdouble(sig)) ** 2)
+        F = np.cumsum(w) / np.sum(w)
+        for j in rng.choice(len(F) - 1, 3):
+            for eps in (-1e-6, -1e-9, -1e-11, -1e-13, 1e-13, 1e-11, 1e-9, 1e-6):
+                u = float(F[j]) + eps
+                if 0.0 <= u < 1.0:
+                    mus.append(mu), sigs.append(sig), us.append(u)
+    mu, sig, u = np.array(mus), np.array(sigs), np.array(us)
+    z_t, ln_t = ctx.sample_z(mu, sig, u, table=True)
+    for mode in (None, "decision", "libm", "libm_decision"):
+        z, ln = ctx.sample_z(mu, sig, u, mode=mode)
+        assert np.array_equal(z, z_t), mode
+        if mode in (None, "libm"):
+            np.testing.assert_allclose(ln, ln_t, rtol=1e-13, atol=1e-13)
+
+
+def test_samplez_tab_vs_libm_random(ctx):
+    """Tabulated erf/exp path vs ocml libm path vs table walk on 400k random draws
+    over sigma in [4, 1e6] (wide windows, capped and uncapped)."""
+    rng = np.random.default_rng(78)
+    n = 400000
+    sig = np.exp(rng.uniform(np.log(4.0), np.log(1e6), n))
+    mu = rng.uniform(-1, 1, n) * rng.choice([1.0, 30.0, 1e4, 1e9], n)
+    u = rng.random(n)
+    z_t, _ = ctx.sample_z(mu, sig, u, table=True)
+    z_d, _ = ctx.sample_z(mu, sig, u, mode="decision")
+    z_l, _ = ctx.sample_z(mu, sig, u, mode="libm_decision")
+    assert np.array_equal(z_d, z_t)
+    assert np.array_equal(z_l, z_t)
 
 
 def test_samplez_em_vs_table_vs_oracle_stress(ctx, oracle):
