@@ -93,6 +93,7 @@ struct lgs_ctx {
     int panel = 32;
     bool has_B = false;
     DevBuf R, RP, RC, BT, coord;  // coord: cp | rii | sig | sig_ref | lterm | irii | ros | isr
+    DevBuf RS, RX;                // 32-row panels: 16-row sub-panel columns, coupling blocks
     DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
     DevBuf etab;                  // SampleZ erf/exp table (lgs_device.h erf_gauss)
     DevBuf szc;                   // per-coordinate SampleZ constants (lgs_kernels.h kSzc*)
@@ -226,6 +227,8 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
     a.flags = c->flags.as<unsigned int>();
     a.etab = c->libm_samplez ? nullptr : c->etab.as<double>();
     a.szc = c->libm_samplez ? nullptr : c->szc.as<double>();
+    a.rs16 = c->RS.as<double>();
+    a.rx = c->RX.as<double>();
     return a;
 }
 
@@ -431,6 +434,31 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
             rcv[(size_t)i * (PB - 1) + m] = row >= p_lo ? R[(size_t)row * dd + i] : 0.0;
         }
     }
+    // 32-row panels, two-level near field (klein_mfma_kernel): RS = near-field
+    // columns of 16-row sub-panels, RX = per panel the block R[p_hi-32+nq][p_hi-16+4kk+kq]
+    // in MFMA A-fragment order [kk][lane = 16 kq + nq] (0 for rows < 0)
+    std::vector<double> rsv(dd * 15, 0.0), rxv;
+    for (int64_t i = 0; i < d; ++i) {
+        const int64_t sp = (d - 1 - i) / 16;
+        const int64_t s_lo = std::max<int64_t>(0, d - (sp + 1) * 16);
+        for (int m = 0; m < 15; ++m) {
+            const int64_t row = i - 1 - m;
+            rsv[(size_t)i * 15 + m] = row >= s_lo ? R[(size_t)row * dd + i] : 0.0;
+        }
+    }
+    rxv.assign((size_t)256 * ((d + 31) / 32), 0.0);
+    for (int64_t pk = 0; pk < (d + 31) / 32; ++pk) {
+        const int64_t p_hi = d - 32 * pk;
+        for (int kk = 0; kk < 4; ++kk)
+            for (int l = 0; l < 64; ++l) {
+                const int64_t row = p_hi - 32 + (l & 15), col = p_hi - 16 + 4 * kk + (l >> 4);
+                if (row >= 0 && col >= 0 && col < d)
+                    rxv[(size_t)pk * 256 + kk * 64 + l] = R[(size_t)row * dd + col];
+            }
+    }
+    if ((rc = c->RS.reserve(rsv.size() * 8)) || (rc = c->RX.reserve(rxv.size() * 8))) return rc;
+    HIP_TRY(hipMemcpy(c->RS.p, rsv.data(), rsv.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->RX.p, rxv.data(), rxv.size() * 8, hipMemcpyHostToDevice));
     if ((rc = c->R.reserve(dd * dd * 8)) || (rc = c->RP.reserve(rp.size() * 8)) ||
         (rc = c->RC.reserve(rcv.size() * 8)) || (rc = c->coord.reserve(co.size() * 8)) ||
         (rc = c->szc.reserve(szc.size() * 8)))

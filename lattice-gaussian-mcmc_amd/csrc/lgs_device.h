@@ -16,6 +16,13 @@
 
 namespace lgs {
 
+// Basis constants are never written by a kernel: reading them through the
+// constant address space lets wave-uniform loads be scalar (s_load).  Through a
+// generic pointer the compiler cannot rule out aliasing with the coefficient
+// stores and issues vector (or flat) loads with a full-latency wait each.
+using cdptr = const __attribute__((address_space(4))) double*;
+__device__ __forceinline__ cdptr cst(const double* p) { return (cdptr)p; }
+
 constexpr uint32_t kTagCoord = 0;
 constexpr uint32_t kTagAccept = 1;
 
@@ -449,8 +456,8 @@ __device__ __forceinline__ double em_C_rel(double kd, double m, double sig, doub
     return em_P_tab<NT>(kd, m, sig, is, etab, fk) + 0.5 * fk - base;
 }
 
-template <int NT, typename TP>
-__device__ __forceinline__ double sample_z_wide(double mu, double u, const double* __restrict__ q,
+template <int NT, typename TP, typename QP>
+__device__ __forceinline__ double sample_z_wide(double mu, double u, QP q,
                                                 int kind, int precision, bool linear_probs,
                                                 bool want_log, TP etab, double& log_norm) {
     const double sig = q[0], is = q[1];
@@ -514,7 +521,11 @@ template <typename TP>
 LGS_SAMPLEZ_ATTR double sample_z_coord(double mu, double u, const double* __restrict__ qv,
                                        int precision, bool linear_probs, bool want_log, TP etab,
                                        double& log_norm) {
-    const double* __restrict__ q = uniform_ptr(qv);  // all lanes are on the same coordinate
+#ifdef LGS_Q_VMEM
+    const double* __restrict__ q = uniform_ptr(qv);
+#else
+    const cdptr q = cst(uniform_ptr(qv));  // all lanes are on the same coordinate
+#endif
     const int kind = (int)q[2];
     const double sig = q[0];
     if (kind == kSzSmall) {
@@ -526,6 +537,18 @@ LGS_SAMPLEZ_ATTR double sample_z_coord(double mu, double u, const double* __rest
             return (double)o.z;
         }
         const double is = q[1];
+        if (hi - lo == 1.0) {
+            // two points whose weights differ by more than e^745.2: the smaller
+            // one is exactly 0 in fp64 (as in the general loop below), so the
+            // decision is the heavier point for every u
+            const double t0 = (lo - mu) * is, t1 = (hi - mu) * is;
+            const double e0 = -0.5 * (t0 * t0), e1 = -0.5 * (t1 * t1);
+            const double em = fmax(e0, e1);
+            if (fmin(e0, e1) - em < -745.2 && !(linear_probs && em < -745.2)) {
+                log_norm = want_log ? em : 0.0;
+                return e0 > e1 ? lo : hi;
+            }
+        }
         double e[4];
         double emax = -INFINITY;
 #pragma unroll

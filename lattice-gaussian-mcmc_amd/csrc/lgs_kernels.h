@@ -21,7 +21,7 @@ constexpr int kErfTabLast = 512;  // SampleZ erf/exp table: y_j = j/64, j = 0..k
 //   [9..9+kSzDeg] / [20..20+kSzDeg]: monomial coefficients in m = mu - rint(mu)
 //   of S(m) / base(m) (kind kSzCapped)
 constexpr int kSzcStride = 32;
-constexpr int kSzDeg = 10;
+constexpr int kSzDeg = 5;  // degree 4 already reaches the fp64 floor for sigma in [50, 1e6]
 constexpr int kSzRound = 0;    // sigma_i < 1e-10: round(mu), no draw
 constexpr int kSzSmall = 1;    // sigma_i < 4: <= 4-point exponent path / table walk
 constexpr int kSzClosed = 2;   // uncapped window of +-rf*sigma, rf >= 9: S = 2 sc, base = -sc
@@ -66,6 +66,8 @@ struct KleinArgs {
     unsigned int* flags;
     const double* etab;  // SampleZ erf/exp table (nullptr: ocml libm path)
     const double* szc;   // per-coordinate SampleZ constants (nullptr: generic sample_z)
+    const double* rs16;  // 16-row sub-panel near-field columns (RC layout of 16-row panels)
+    const double* rx;    // per 32-row panel: 16x16 block R[p_hi-32.., p_hi-16..] as MFMA A fragments
 };
 
 struct AcceptArgs {

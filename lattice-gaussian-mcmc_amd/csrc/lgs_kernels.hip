@@ -46,9 +46,14 @@ __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double
         flags |= kFlagNonFinite;
         return 0.0;
     }
-    const double s = a.szc ? a.szc[(size_t)i * kSzcStride] : a.sig[i];
+    const double s = a.szc ? cst(a.szc)[(size_t)i * kSzcStride] : cst(a.sig)[i];
 #ifdef LGS_DIAG_NO_SAMPLEZ
     if (true) {  // diagnostic build: SampleZ replaced by rounding
+        zi = rint(mu + rs.u((uint32_t)(a.d - 1 - i)) * 1e-300);
+    } else
+#endif
+#ifdef LGS_DIAG_SZ_KIND_ONLY
+    if (a.szc && (int)cst(a.szc)[(size_t)i * kSzcStride + 2] != LGS_DIAG_SZ_KIND_ONLY) {
         zi = rint(mu + rs.u((uint32_t)(a.d - 1 - i)) * 1e-300);
     } else
 #endif
@@ -69,9 +74,9 @@ __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double
         // Reference-mode importance weight (imhk.py:102-124): log_gaussian_weight(Bz)
         // - compute_log_density(Bz), with ||Bz - c||^2 = sum_i (R_ii (z_i - mu_i))^2.
         const double res = zi - mu;
-        const double ta = res * a.ros[i];
-        const double tq = res * a.isr[i];
-        lw += (-0.5 * (ta * ta)) - (-0.5 * (tq * tq) - a.lterm[i]);
+        const double ta = res * cst(a.ros)[i];
+        const double tq = res * cst(a.isr)[i];
+        lw += (-0.5 * (ta * ta)) - (-0.5 * (tq * tq) - cst(a.lterm)[i]);
     }
     return zi;
 }
@@ -175,11 +180,11 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
         }
         for (int s = 0; s < rows; ++s) {
             const int i = p_hi - 1 - s;
-            const double mu = (a.cp[i] - acc[PB - 1]) * a.irii[i];
+            const double mu = (cst(a.cp)[i] - acc[PB - 1]) * cst(a.irii)[i];
             const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s);
             store_z(Z, (size_t)i * ldz + p, zi, flags);
             const double x = zi;
-            const double* __restrict__ rc = RC + (size_t)i * (PB - 1);
+            const cdptr rc = cst(RC) + (size_t)i * (PB - 1);
 #pragma unroll
             for (int k = 0; k < PB - 1; ++k) acc[k] = fma(rc[PB - 2 - k], x, acc[k]);
 #pragma unroll
@@ -240,7 +245,7 @@ struct ZQuad<int64_t> {
 
 template <typename ZT, int PB, bool WL>
 #ifndef LGS_MFMA_LB32
-#define LGS_MFMA_LB32 2
+#define LGS_MFMA_LB32 3
 #endif
 __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_kernel(const KleinArgs a,
                                                             const double* __restrict__ RP,
@@ -253,6 +258,12 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t p0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
     if (p0 >= a.n) return;  // whole waves only (n % 64 == 0)
+#ifdef LGS_STAGGER
+    {  // diagnostic: desynchronise co-resident blocks
+        const unsigned h = (blockIdx.x * 2654435761u) >> 16;
+        for (unsigned it = 0; it < (h % 3) * LGS_STAGGER; ++it) __builtin_amdgcn_s_sleep(127);
+    }
+#endif
     const int64_t p = p0 + lane;
     uint32_t chain, step;
     lane_counter(a, p, chain, step);
@@ -265,7 +276,8 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
     const int npan = (d + PB - 1) / PB;
     double* F = Fl[wave];
     const int kq = lane >> 4, nq = lane & 15;
-    double acc[PB];
+    constexpr int NACC = PB == 32 ? 16 : PB;  // running sums live across SampleZ calls
+    double acc[NACC];
     for (int pk = 0; pk < npan; ++pk) {
         const int p_hi = d - pk * PB;
         const int rows = p_hi < PB ? p_hi : PB;
@@ -327,36 +339,113 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
             }
 #pragma unroll
             for (int st = 0; st < 4; ++st) consume(st);
-            // D -> LDS [row][chain] -> one chain per lane, one 16-row tile at a time
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
+            if constexpr (PB == 32) {
+                // tile 1 (rows p_hi-16..p_hi-1) -> acc; tile 0 stays in LDS for the
+                // second sub-panel
 #pragma unroll
                 for (int g = 0; g < 4; ++g)
 #pragma unroll
-                    for (int reg = 0; reg < 4; ++reg) F[(kq + 4 * reg) * LDF + 4 * nq + g] = f[t][g][reg];
+                    for (int reg = 0; reg < 4; ++reg) F[(kq + 4 * reg) * LDF + 4 * nq + g] = f[1][g][reg];
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 __builtin_amdgcn_wave_barrier();
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[16 * t + r] = F[r * LDF + lane];
+                for (int r = 0; r < 16; ++r) acc[r] = F[r * LDF + lane];
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg) F[(kq + 4 * reg) * LDF + 4 * nq + g] = f[0][g][reg];
+            } else {
+                // D -> LDS [row][chain] -> one chain per lane, one 16-row tile at a time
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+#pragma unroll
+                        for (int reg = 0; reg < 4; ++reg) F[(kq + 4 * reg) * LDF + 4 * nq + g] = f[t][g][reg];
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[16 * t + r] = F[r * LDF + lane];
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
             }
         } else {
 #pragma unroll
-            for (int r = 0; r < PB; ++r) acc[r] = 0.0;
+            for (int r = 0; r < NACC; ++r) acc[r] = 0.0;
+            if constexpr (PB == 32) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) F[r * LDF + lane] = 0.0;
+            }
         }
-        for (int s = 0; s < rows; ++s) {
-            const int i = p_hi - 1 - s;
-            const double mu = (a.cp[i] - acc[PB - 1]) * a.irii[i];
-            const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s);
-            store_z(Z, (size_t)i * ldz + p, zi, flags);
-            const double x = zi;
-            const double* __restrict__ rc = RC + (size_t)i * (PB - 1);
+        if constexpr (PB == 32) {
+            // Two-level near field: the 32-row panel is decided as two 16-row
+            // sub-panels, so only 16 running sums are live across the SampleZ
+            // calls (occupancy); the block R[L rows, U cols] that couples them is
+            // applied with 16 MFMAs after the upper sub-panel U is decided.
+            auto near16 = [&](int rows16, int top) {
+                for (int s = 0; s < rows16; ++s) {
+                    // i is wave-uniform; say so, or the per-coordinate constants
+                    // are fetched with vector loads and a full-latency wait per row
+                    const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
+                    const double mu = (cst(a.cp)[i] - acc[15]) * cst(a.irii)[i];
+                    const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s);
+                    store_z(Z, (size_t)i * ldz + p, zi, flags);
+                    const cdptr rc = cst(a.rs16) + (size_t)i * 15;
 #pragma unroll
-            for (int k = 0; k < PB - 1; ++k) acc[k] = fma(rc[PB - 2 - k], x, acc[k]);
+                    for (int k = 0; k < 15; ++k) acc[k] = fma(rc[14 - k], zi, acc[k]);
 #pragma unroll
-            for (int k = PB - 1; k >= 1; --k) acc[k] = acc[k - 1];
-            acc[0] = 0.0;
+                    for (int k = 15; k >= 1; --k) acc[k] = acc[k - 1];
+                    acc[0] = 0.0;
+                }
+            };
+            near16(p_hi < 16 ? p_hi : 16, p_hi);
+            const int rows_l = p_hi - 16 < 16 ? p_hi - 16 : 16;
+            if (rows_l > 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                d4_t c[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) c[g] = (d4_t){0.0, 0.0, 0.0, 0.0};
+                const double* __restrict__ rx = a.rx + (size_t)pk * 256 + lane;
+                const ZT* __restrict__ zu = Z + p0 + (size_t)(p_hi - 16) * ldz + (size_t)kq * ldz + 4 * nq;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const double av = rx[64 * kk];
+                    ZQuad<ZT> q;
+                    q.load(zu + (size_t)(4 * kk) * ldz);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        c[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, q.get(g), c[g], 0, 0, 0);
+                }
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg) F[(kq + 4 * reg) * LDF + 4 * nq + g] += c[g][reg];
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] = F[r * LDF + lane];
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                near16(rows_l, p_hi - 16);
+            }
+        } else {
+            for (int s = 0; s < rows; ++s) {
+                const int i = p_hi - 1 - s;
+                const double mu = (cst(a.cp)[i] - acc[PB - 1]) * cst(a.irii)[i];
+                const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s);
+                store_z(Z, (size_t)i * ldz + p, zi, flags);
+                const double x = zi;
+                const cdptr rc = cst(RC) + (size_t)i * (PB - 1);
+#pragma unroll
+                for (int k = 0; k < PB - 1; ++k) acc[k] = fma(rc[PB - 2 - k], x, acc[k]);
+#pragma unroll
+                for (int k = PB - 1; k >= 1; --k) acc[k] = acc[k - 1];
+                acc[0] = 0.0;
+            }
         }
     }
     if (a.LW) a.LW[p] = lw;
