@@ -93,7 +93,7 @@ struct lgs_ctx {
     int panel = 32;
     bool has_B = false;
     DevBuf R, RP, RC, BT, coord;  // coord: cp | rii | sig | sig_ref | lterm | irii | ros | isr
-    DevBuf RS, RX;                // 32-row panels: 16-row sub-panel columns, coupling blocks
+    DevBuf CREC, RX;              // 32-row panels: per-coordinate records, coupling blocks
     DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
     DevBuf etab;                  // SampleZ erf/exp table (lgs_device.h erf_gauss)
     DevBuf szc;                   // per-coordinate SampleZ constants (lgs_kernels.h kSzc*)
@@ -227,7 +227,7 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
     a.flags = c->flags.as<unsigned int>();
     a.etab = c->libm_samplez ? nullptr : c->etab.as<double>();
     a.szc = c->libm_samplez ? nullptr : c->szc.as<double>();
-    a.rs16 = c->RS.as<double>();
+    a.crec = c->CREC.as<double>();
     a.rx = c->RX.as<double>();
     return a;
 }
@@ -456,8 +456,20 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
                     rxv[(size_t)pk * 256 + kk * 64 + l] = R[(size_t)row * dd + col];
             }
     }
-    if ((rc = c->RS.reserve(rsv.size() * 8)) || (rc = c->RX.reserve(rxv.size() * 8))) return rc;
-    HIP_TRY(hipMemcpy(c->RS.p, rsv.data(), rsv.size() * 8, hipMemcpyHostToDevice));
+    // per-coordinate records (lgs_kernels.h kRec*)
+    std::vector<double> crec(dd * lgs::kRecStride, 0.0);
+    for (size_t i = 0; i < dd; ++i) {
+        double* r = crec.data() + i * lgs::kRecStride;
+        std::copy(szc.data() + i * lgs::kSzcStride, szc.data() + i * lgs::kSzcStride + lgs::kSzUsed, r);
+        r[lgs::kRecCp] = co[i];
+        r[lgs::kRecIrii] = co[5 * dd + i];
+        r[lgs::kRecRos] = co[6 * dd + i];
+        r[lgs::kRecIsr] = co[7 * dd + i];
+        r[lgs::kRecLterm] = co[4 * dd + i];
+        std::copy(rsv.data() + i * 15, rsv.data() + i * 15 + 15, r + lgs::kRecRs);
+    }
+    if ((rc = c->CREC.reserve(crec.size() * 8)) || (rc = c->RX.reserve(rxv.size() * 8))) return rc;
+    HIP_TRY(hipMemcpy(c->CREC.p, crec.data(), crec.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->RX.p, rxv.data(), rxv.size() * 8, hipMemcpyHostToDevice));
     if ((rc = c->R.reserve(dd * dd * 8)) || (rc = c->RP.reserve(rp.size() * 8)) ||
         (rc = c->RC.reserve(rcv.size() * 8)) || (rc = c->coord.reserve(co.size() * 8)) ||

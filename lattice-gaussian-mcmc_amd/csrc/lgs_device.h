@@ -465,12 +465,12 @@ __device__ __forceinline__ double sample_z_wide(double mu, double u, QP q,
     const double m = mu - c;
     double S, base, a, b;
     if (kind == kSzCapped) {
-        S = q[9 + kSzDeg];
-        base = q[20 + kSzDeg];
+        S = q[kSzS + kSzDeg];
+        base = q[kSzB + kSzDeg];
 #pragma unroll
         for (int k = kSzDeg - 1; k >= 0; --k) {
-            S = fma(S, m, q[9 + k]);
-            base = fma(base, m, q[20 + k]);
+            S = fma(S, m, q[kSzS + k]);
+            base = fma(base, m, q[kSzB + k]);
         }
         a = -500.0;
         b = 500.0;
@@ -487,11 +487,13 @@ __device__ __forceinline__ double sample_z_wide(double mu, double u, QP q,
     double kd = fmin(fmax((double)ceilf(xg - 0.5f), a), b);
     double fk;
     double Ck = em_C_rel<NT>(kd, m, sig, is, etab, base, fk);
+#pragma nounroll
     for (int it = 0; it < 64 && Ck <= target && kd < b; ++it) {  // move up
         kd += 1.0;
         fk = gauss_tab(kd, m, is, etab);
         Ck += fk;
     }
+#pragma nounroll
     for (int it = 0; it < 64 && kd > a && Ck - fk > target; ++it) {  // move down
         Ck -= fk;
         kd -= 1.0;
@@ -507,6 +509,19 @@ __device__ __forceinline__ double sample_z_wide(double mu, double u, QP q,
     return c + kd;
 }
 
+// Both window ends evaluated per draw (kinds without precomputed normalisers);
+// out of line: its two concurrent erf evaluations would otherwise set the
+// register footprint of sample_z_coord.
+template <typename TP>
+__device__ __noinline__ SampleZOut sample_z_generic(double mu, double sig, int precision,
+                                                    bool linear_probs, double u, bool want_log,
+                                                    TP etab) {
+    int64_t lo, hi;
+    support_window(mu, sig, precision, lo, hi);
+    return sig < 50.0 ? sample_z_em_tab<6>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab)
+                      : sample_z_em_tab<3>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab);
+}
+
 // A wave-uniform pointer passed to a non-inlined function arrives in VGPRs;
 // readfirstlane makes it scalar so its loads are s_load into SGPRs.
 template <typename T>
@@ -517,15 +532,21 @@ __device__ __forceinline__ const T* uniform_ptr(const T* p) {
     return (const T*)(((uint64_t)hi << 32) | lo);
 }
 
-template <typename TP>
-LGS_SAMPLEZ_ATTR double sample_z_coord(double mu, double u, const double* __restrict__ qv,
-                                       int precision, bool linear_probs, bool want_log, TP etab,
+// Per-coordinate constants arrive either as a constant-address-space pointer
+// (made scalar inside the callee) or as an LDS pointer (records staged per panel).
+__device__ __forceinline__ cdptr uniformize(cdptr p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (cdptr)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ lds_cdptr uniformize(lds_cdptr p) { return p; }
+
+template <typename TP, typename QP>
+LGS_SAMPLEZ_ATTR double sample_z_coord(double mu, double u, QP qin, int precision,
+                                       bool linear_probs, bool want_log, TP etab,
                                        double& log_norm) {
-#ifdef LGS_Q_VMEM
-    const double* __restrict__ q = uniform_ptr(qv);
-#else
-    const cdptr q = cst(uniform_ptr(qv));  // all lanes are on the same coordinate
-#endif
+    const QP q = uniformize(qin);  // all lanes are on the same coordinate
     const int kind = (int)q[2];
     const double sig = q[0];
     if (kind == kSzSmall) {
@@ -584,12 +605,7 @@ LGS_SAMPLEZ_ATTR double sample_z_coord(double mu, double u, const double* __rest
         return z;
     }
     if (kind == kSzGeneric) {
-        int64_t lo, hi;
-        support_window(mu, sig, precision, lo, hi);
-        const SampleZOut o =
-            sig < 50.0
-                ? sample_z_em_tab<6>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab)
-                : sample_z_em_tab<3>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab);
+        const SampleZOut o = sample_z_generic(mu, sig, precision, linear_probs, u, want_log, etab);
         log_norm = o.log_norm;
         return (double)o.z;
     }

@@ -18,10 +18,20 @@ constexpr int kErfTabLast = 512;  // SampleZ erf/exp table: y_j = j/64, j = 0..k
 //   [0] sigma_i  [1] 1/sigma_i  [2] kind  [3] sc = sigma*sqrt(pi/2)  [4] 1/sc
 //   [5] sigma*sqrt(2)  [6] rf*sigma (window half-width, klein.py:113-120)
 //   [7] S, [8] base (kind kSzClosed)
-//   [9..9+kSzDeg] / [20..20+kSzDeg]: monomial coefficients in m = mu - rint(mu)
-//   of S(m) / base(m) (kind kSzCapped)
-constexpr int kSzcStride = 32;
+//   [kSzS..kSzS+kSzDeg] / [kSzB..kSzB+kSzDeg]: monomial coefficients in
+//   m = mu - rint(mu) of S(m) / base(m) (kind kSzCapped)
 constexpr int kSzDeg = 5;  // degree 4 already reaches the fp64 floor for sigma in [50, 1e6]
+constexpr int kSzS = 9;
+constexpr int kSzB = kSzS + kSzDeg + 1;
+constexpr int kSzUsed = kSzB + kSzDeg + 1;  // 21
+constexpr int kSzcStride = 24;
+// Klein-path record per coordinate (kRecStride doubles): the SampleZ constants
+// [0, kSzUsed), then c', 1/R_ii, R_ii/sigma, 1/sigma_i^ref, lterm, and the 15
+// near-field coefficients R[i-1-m][i] of the coordinate's 16-row sub-panel.
+// Staged into LDS once per 32-row panel by klein_mfma_kernel.
+constexpr int kRecCp = kSzUsed, kRecIrii = kSzUsed + 1, kRecRos = kSzUsed + 2,
+              kRecIsr = kSzUsed + 3, kRecLterm = kSzUsed + 4, kRecRs = kSzUsed + 5;
+constexpr int kRecStride = kRecRs + 16;  // 42 (one pad): 336 bytes, 16-byte multiple
 constexpr int kSzRound = 0;    // sigma_i < 1e-10: round(mu), no draw
 constexpr int kSzSmall = 1;    // sigma_i < 4: <= 4-point exponent path / table walk
 constexpr int kSzClosed = 2;   // uncapped window of +-rf*sigma, rf >= 9: S = 2 sc, base = -sc
@@ -66,7 +76,7 @@ struct KleinArgs {
     unsigned int* flags;
     const double* etab;  // SampleZ erf/exp table (nullptr: ocml libm path)
     const double* szc;   // per-coordinate SampleZ constants (nullptr: generic sample_z)
-    const double* rs16;  // 16-row sub-panel near-field columns (RC layout of 16-row panels)
+    const double* crec;  // per-coordinate records (kRecStride doubles, layout above)
     const double* rx;    // per 32-row panel: 16x16 block R[p_hi-32.., p_hi-16..] as MFMA A fragments
 };
 

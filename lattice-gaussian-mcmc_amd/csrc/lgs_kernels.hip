@@ -61,7 +61,7 @@ __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double
         zi = rint(mu);
     } else if (a.szc) {
         double ln;
-        zi = sample_z_coord(mu, rs.u((uint32_t)(a.d - 1 - i)), a.szc + (size_t)i * kSzcStride,
+        zi = sample_z_coord(mu, rs.u((uint32_t)(a.d - 1 - i)), cst(a.szc) + (size_t)i * kSzcStride,
                             a.precision, a.linear_probs != 0, WL, etab, ln);
         if (WL) lw += ln;
     } else {
@@ -77,6 +77,49 @@ __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double
         const double ta = res * cst(a.ros)[i];
         const double tq = res * cst(a.isr)[i];
         lw += (-0.5 * (ta * ta)) - (-0.5 * (tq * tq) - cst(a.lterm)[i]);
+    }
+    return zi;
+}
+
+// decide_coord with the coordinate's record rec staged in LDS (klein_mfma_kernel, 32-row panels).
+template <bool WL, typename TP>
+__device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, double mu,
+                                                   lds_cdptr rec, CoordStream& rs, double& lw,
+                                                   unsigned int& flags, TP etab) {
+    double zi;
+    if (!isfinite(mu)) {
+        flags |= kFlagNonFinite;
+        return 0.0;
+    }
+    const double s = rec[0];
+#ifdef LGS_DIAG_NO_SAMPLEZ
+    if (true) {
+        zi = rint(mu + rs.u((uint32_t)(a.d - 1 - i)) * 1e-300);
+    } else
+#endif
+#ifdef LGS_DIAG_SZ_KIND_ONLY
+    if ((int)rec[2] != LGS_DIAG_SZ_KIND_ONLY) {
+        zi = rint(mu + rs.u((uint32_t)(a.d - 1 - i)) * 1e-300);
+    } else
+#endif
+    if (s == 0.0) {
+        zi = rint(mu);
+    } else if (!a.szc) {  // LGS_SAMPLEZ_LIBM: generic path
+        SampleZOut o = sample_z(mu, s, a.precision, a.linear_probs != 0,
+                                rs.u((uint32_t)(a.d - 1 - i)), WL, a.etab);
+        zi = (double)o.z;
+        if (WL) lw += o.log_norm;
+    } else {
+        double ln;
+        zi = sample_z_coord(mu, rs.u((uint32_t)(a.d - 1 - i)), rec, a.precision,
+                            a.linear_probs != 0, WL, etab, ln);
+        if (WL) lw += ln;
+    }
+    if (!WL) {
+        const double res = zi - mu;
+        const double ta = res * rec[kRecRos];
+        const double tq = res * rec[kRecIsr];
+        lw += (-0.5 * (ta * ta)) - (-0.5 * (tq * tq) - rec[kRecLterm]);
     }
     return zi;
 }
@@ -255,15 +298,12 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
     __shared__ double Fl[4][16 * LDF];
     __shared__ double tab_lds[2 * (kErfTabLast + 1)];
     const lds_cdptr etab_s = stage_etab(tab_lds, a.etab);
+    // 32-row panels: the panel's per-coordinate records, staged block-wide
+    __shared__ double rec_lds[PB == 32 ? 32 * kRecStride : 2];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t p0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
-    if (p0 >= a.n) return;  // whole waves only (n % 64 == 0)
-#ifdef LGS_STAGGER
-    {  // diagnostic: desynchronise co-resident blocks
-        const unsigned h = (blockIdx.x * 2654435761u) >> 16;
-        for (unsigned it = 0; it < (h % 3) * LGS_STAGGER; ++it) __builtin_amdgcn_s_sleep(127);
-    }
-#endif
+    const bool active = p0 < a.n;  // whole waves only (n % 64 == 0)
+    if (!active && PB != 32) return;  // (32-row panels: idle waves still stage records)
     const int64_t p = p0 + lane;
     uint32_t chain, step;
     lane_counter(a, p, chain, step);
@@ -281,6 +321,17 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
     for (int pk = 0; pk < npan; ++pk) {
         const int p_hi = d - pk * PB;
         const int rows = p_hi < PB ? p_hi : PB;
+        if constexpr (PB == 32) {
+            // records of coordinates r0 .. r0+31 (r0 = p_hi - 32; negative ones skipped)
+            __syncthreads();
+            const int r0 = p_hi - 32;
+            const double2* __restrict__ src = (const double2*)a.crec;
+            double2* dst = (double2*)rec_lds;
+            for (int e = threadIdx.x; e < 32 * kRecStride / 2; e += 256)
+                if (r0 * (kRecStride / 2) + e >= 0) dst[e] = src[(int64_t)r0 * (kRecStride / 2) + e];
+            __syncthreads();
+            if (!active) continue;
+        }
 #ifdef LGS_DIAG_NO_FAR
         if (false) {
 #else
@@ -387,13 +438,12 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
             // applied with 16 MFMAs after the upper sub-panel U is decided.
             auto near16 = [&](int rows16, int top) {
                 for (int s = 0; s < rows16; ++s) {
-                    // i is wave-uniform; say so, or the per-coordinate constants
-                    // are fetched with vector loads and a full-latency wait per row
                     const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
-                    const double mu = (cst(a.cp)[i] - acc[15]) * cst(a.irii)[i];
-                    const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s);
+                    const lds_cdptr rec = (lds_cdptr)rec_lds + (i - (p_hi - 32)) * kRecStride;
+                    const double mu = (rec[kRecCp] - acc[15]) * rec[kRecIrii];
+                    const double zi = decide_coord_rec<WL>(a, i, mu, rec, rs, lw, flags, etab_s);
                     store_z(Z, (size_t)i * ldz + p, zi, flags);
-                    const cdptr rc = cst(a.rs16) + (size_t)i * 15;
+                    const lds_cdptr rc = rec + kRecRs;
 #pragma unroll
                     for (int k = 0; k < 15; ++k) acc[k] = fma(rc[14 - k], zi, acc[k]);
 #pragma unroll
@@ -448,6 +498,7 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
             }
         }
     }
+    if (!active) return;
     if (a.LW) a.LW[p] = lw;
     if (flags) atomicOr(a.flags, flags);
 }

@@ -105,8 +105,8 @@ inline void build_szc(double s, int precision, double* q) {
         }
     long double scale = 1.0L;
     for (int k = 0; k < N; ++k) {
-        q[9 + k] = (double)(cs[k] * scale);
-        q[20 + k] = (double)(cb[k] * scale);
+        q[lgs::kSzS + k] = (double)(cs[k] * scale);
+        q[lgs::kSzB + k] = (double)(cb[k] * scale);
         scale *= 2.0L;
     }
     // check the fp64 Horner evaluation against long double at 33 points; a fit that
@@ -116,10 +116,10 @@ inline void build_szc(double s, int precision, double* q) {
         const double m = -0.5 + t / 32.0;
         long double Se, be;
         capped_S_base(m, sg, Se, be);
-        double S = q[9 + lgs::kSzDeg], b = q[20 + lgs::kSzDeg];
+        double S = q[lgs::kSzS + lgs::kSzDeg], b = q[lgs::kSzB + lgs::kSzDeg];
         for (int k = lgs::kSzDeg - 1; k >= 0; --k) {
-            S = std::fma(S, m, q[9 + k]);
-            b = std::fma(b, m, q[20 + k]);
+            S = std::fma(S, m, q[lgs::kSzS + k]);
+            b = std::fma(b, m, q[lgs::kSzB + k]);
         }
         err = std::max(err, std::max(fabsl((long double)S - Se), fabsl((long double)b - be)));
         Smin = std::min(Smin, Se);
