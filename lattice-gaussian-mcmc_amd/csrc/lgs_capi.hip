@@ -77,6 +77,7 @@ struct BzCall {  // an int8-digit B z launch, replayed in fp64 if a digit overfl
     int64_t ldz, n;
     double* V;
     int64_t rb, rstride, roff;
+    const int64_t* sel;  // nullable: sample s reads column sel[s] of Z
 };
 
 }  // namespace
@@ -95,6 +96,7 @@ struct lgs_ctx {
     DevBuf R, RP, RC, BT, coord;  // coord: cp | rii | sig | sig_ref | lterm | irii | ros | isr
     DevBuf CREC, RX;              // 32-row panels: per-coordinate records, coupling blocks
     DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
+    DevBuf kchunk, koff;          // per 128-row tile of B: the 64-column chunks with a non-zero digit
     DevBuf etab;                  // SampleZ erf/exp table (lgs_device.h erf_gauss)
     DevBuf szc;                   // per-coordinate SampleZ constants (lgs_kernels.h kSzc*)
     bool libm_samplez = false;    // LGS_SAMPLEZ_LIBM=1: ocml erf/exp/erfinv path instead
@@ -268,7 +270,7 @@ int run_klein_store(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int& zb,
 
 int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
     Scope s(c, 1);
-    HIP_TRY(lgs::launch::bz(b.Z, b.zb, b.ldz, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
+    HIP_TRY(lgs::launch::bz(b.Z, b.zb, b.ldz, b.sel, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
                             b.rstride, b.roff, c->stream));
     return LGS_OK;
 }
@@ -276,15 +278,16 @@ int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
 // v = B z: exact int8-digit MFMA kernel for integer bases (fp64 replay on digit
 // overflow, see finish()), fp64 MFMA kernel otherwise.  LGS_BZ_FP64=1 forces fp64.
 int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
-           int64_t rb = 0, int64_t rstride = 0, int64_t roff = 0) {
+           int64_t rb = 0, int64_t rstride = 0, int64_t roff = 0, const int64_t* sel = nullptr) {
     if (!c->has_B) return fail(LGS_ERR_STATE, "lattice points need B (lgs_set_basis B != NULL)");
-    BzCall b{Z, zb, ldz, n, V, rb > 0 ? rb : n, rstride, roff};
+    BzCall b{Z, zb, ldz, n, V, rb > 0 ? rb : n, rstride, roff, sel};
     static const bool force64 = getenv("LGS_BZ_FP64") && atoi(getenv("LGS_BZ_FP64")) == 1;
     if (!c->has_Bi8 || force64) return run_bz_fp64(c, b);
     Scope s(c, 1);
     const int8_t* hi = c->Bd.as<int8_t>();
     const int8_t* lo = hi + (size_t)c->bd_rows * c->bd_cols;
-    HIP_TRY(lgs::launch::bz_i8(Z, zb, ldz, hi, lo, (int)c->bd_cols, (int)c->d, n, V, c->d, b.rb,
+    HIP_TRY(lgs::launch::bz_i8(Z, zb, ldz, sel, c->kchunk.as<int>(), c->koff.as<int>(), hi, lo,
+                               (int)c->bd_cols, (int)c->d, n, V, c->d, b.rb,
                                b.rstride, b.roff, c->flags.as<unsigned int>(), c->stream));
     c->pending_i8.push_back(b);
     return LGS_OK;
@@ -506,6 +509,23 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
                 }
             if ((rc = c->Bd.reserve(planes.size()))) return rc;
             HIP_TRY(hipMemcpy(c->Bd.p, planes.data(), planes.size(), hipMemcpyHostToDevice));
+            // block sparsity of B for bz_i8_kernel: an all-zero 128 x 64 block contributes
+            // exactly nothing, so its K chunk is skipped (NTRU [[qI,0],[H,I]]: 62% of blocks)
+            std::vector<int> kc, ko(1, 0);
+            for (int64_t rt = 0; rt < rows / 128; ++rt) {
+                for (int64_t ch = 0; ch < cols / 64; ++ch) {
+                    bool nz = false;
+                    for (int64_t r = rt * 128; r < rt * 128 + 128 && !nz; ++r)
+                        for (int64_t k = ch * 64; k < ch * 64 + 64 && !nz; ++k)
+                            nz = hi[r * cols + k] != 0 || lo[r * cols + k] != 0;
+                    if (nz) kc.push_back((int)ch);
+                }
+                ko.push_back((int)kc.size());
+            }
+            if (kc.empty()) kc.push_back(0);
+            if ((rc = c->kchunk.reserve(kc.size() * 4)) || (rc = c->koff.reserve(ko.size() * 4))) return rc;
+            HIP_TRY(hipMemcpy(c->kchunk.p, kc.data(), kc.size() * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(c->koff.p, ko.data(), ko.size() * 4, hipMemcpyHostToDevice));
             c->bd_rows = rows;
             c->bd_cols = cols;
         }
@@ -701,7 +721,11 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
     T = std::min<int64_t>(T, std::max<int64_t>(n_steps, 1));
     const int64_t np = nc * T;
     const int64_t kmax = std::max<int64_t>(T / thin, 1);
-    if ((rc = c->Z.reserve((size_t)np * d * std::max(zb, 4))) || (rc = c->LW.reserve((size_t)np * 8)) ||
+    // proposal store: np columns, plus nc columns for the chain states carried into a
+    // block when lattice points are requested (kept-state selections become plain columns)
+    const bool carry = v_samples != nullptr;
+    if ((rc = c->Z.reserve((size_t)(np + (carry ? nc : 0)) * d * std::max(zb, 4))) ||
+        (rc = c->LW.reserve((size_t)np * 8)) ||
         (rc = c->sel.reserve((size_t)std::max<int64_t>(nc * kmax, nc) * 8)) ||
         (rc = c->fsel.reserve((size_t)nc * 8)) || (rc = c->cnt.reserve((size_t)np * 4)) ||
         (rc = c->ccnt.reserve((size_t)nc * 4)))
@@ -782,11 +806,14 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         a.counter_mode = 1;
         a.chain0 = (uint32_t)first_chain;
         a.step0 = (uint32_t)(first_step + (uint64_t)t0);
+        const int64_t ldzb = npb + (carry ? nc : 0);  // multiple of 4 when nc is
         a.nt = Tb;
         a.n = npb;
-        a.ldz = npb;
+        a.ldz = ldzb;
         a.LW = c->LW.as<double>();
         if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p))) return rc;
+        if (carry && kb > 0)
+            HIP_TRY(lgs::launch::carry_cols(zs, ob, cm, nc, (int)d, c->Z.p, zb, ldzb, npb, c->stream));
         if (moments) HIP_TRY(hipMemsetAsync(c->cnt.p, 0, (size_t)npb * 4, c->stream));
         lgs::AcceptArgs aa{};
         aa.nc = nc;
@@ -801,6 +828,7 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         aa.accepts = acc;
         aa.sel = (z_samples || v_samples) && kb > 0 ? c->sel.as<int64_t>() : nullptr;
         aa.final_sel = c->fsel.as<int64_t>();
+        aa.carry_col = carry ? npb : -1;
         aa.cnt = moments ? c->cnt.as<int32_t>() : nullptr;
         aa.cnt_carry = moments ? c->ccnt.as<int32_t>() : nullptr;
         {
@@ -809,21 +837,23 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         }
         if (moments) {
             Scope s(c, 3);
-            HIP_TRY(lgs::launch::moments(c->Z.p, zb, npb, c->cnt.as<int32_t>(), npb, (int)d, mom, c->stream));
+            HIP_TRY(lgs::launch::moments(c->Z.p, zb, ldzb, c->cnt.as<int32_t>(), npb, (int)d, mom, c->stream));
             HIP_TRY(lgs::launch::moments_carry(zs, ob, cm, nc, (int)d, c->ccnt.as<int32_t>(), mom, c->stream));
         }
         if ((z_samples || v_samples) && kb > 0) {
             // kept states q = chain*kb + k, gathered coordinate-major (d x nq); chain-major
             // proposal order makes this a near-contiguous copy
             const int64_t nq = nc * kb;
-            if ((rc = c->stage_f.reserve((size_t)nq * d * ob))) return rc;
-            HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, npb, c->sel.as<int64_t>(), nq, kb, zs, ob, cm, nc,
-                                          (int)d, c->stage_f.p, 1, c->stream));
-            if (v_samples) {  // rows (chain, first_keep + k) of the n_chains x n_keep x d output
-                if ((rc = run_bz(c, c->stage_f.p, ob, nq, nq, v_samples, kb, n_keep, first_keep)))
+            if (v_samples) {  // rows (chain, first_keep + k) of the n_chains x n_keep x d output,
+                              // read straight from the proposal store through the selections
+                if ((rc = run_bz(c, c->Z.p, zb, ldzb, nq, v_samples, kb, n_keep, first_keep,
+                                 c->sel.as<int64_t>())))
                     return rc;
             }
             if (z_samples) {
+                if ((rc = c->stage_f.reserve((size_t)nq * d * ob))) return rc;
+                HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, ldzb, c->sel.as<int64_t>(), nq, kb, zs, ob, cm,
+                                              nc, (int)d, c->stage_f.p, 1, c->stream));
                 if ((rc = c->stage_g.reserve((size_t)nq * d * ob))) return rc;
                 HIP_TRY(lgs::launch::transpose_out(c->stage_f.p, ob, nq, nq, (int)d, c->stage_g.p,
                                                    ob, c->stream));
@@ -833,7 +863,7 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
             }
         }
         // chain states after the block (in place; carried chains keep their row)
-        HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, npb, c->fsel.as<int64_t>(), nc, 1, zs, ob, cm, nc,
+        HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, ldzb, c->fsel.as<int64_t>(), nc, 1, zs, ob, cm, nc,
                                       (int)d, zs, cm, c->stream));
         if ((rc = finish(c))) return rc;
     }

@@ -95,6 +95,7 @@ struct AcceptArgs {
     int64_t* final_sel;  // nc
     int32_t* cnt;        // nullable, per proposal (zeroed by caller)
     int32_t* cnt_carry;  // nullable, per chain
+    int64_t carry_col;   // >= 0: sel of a state carried in from before the block = carry_col + chain
 };
 
 namespace launch {
@@ -121,10 +122,14 @@ hipError_t transpose_out(const void* Z, int zb, int64_t ldz, int64_t n, int d, v
 hipError_t to_coord_major(const void* in, int ib, int64_t n, int d, void* Z, int zb, int64_t ldz,
                           hipStream_t st);
 // V row of sample s: (s / rb) * rstride + roff + s % rb (rb = n, rstride = roff = 0: row s)
-hipError_t bz(const void* Z, int zb, int64_t ldz, const double* BT, int d, int64_t n, double* V,
-              int64_t ldv, int64_t rb, int64_t rstride, int64_t roff, hipStream_t st);
-hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int8_t* Bd1, const int8_t* Bd0, int dc,
-                 int d, int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
+hipError_t bz(const void* Z, int zb, int64_t ldz, const int64_t* sel, const double* BT, int d,
+              int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
+              hipStream_t st);
+hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const int* kchunk,
+                 const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
+                 double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, hipStream_t st);
+hipError_t carry_cols(const void* zs, int ob, int zs_coord_major, int64_t nc, int d, void* Z, int zb,
+                      int64_t ldz, int64_t col0, hipStream_t st);
 }  // namespace launch
 }  // namespace lgs

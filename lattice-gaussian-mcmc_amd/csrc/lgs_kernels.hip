@@ -582,7 +582,7 @@ __global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
             ++acc;
         }
         if ((t + 1) % a.thin == 0) {
-            if (a.sel) a.sel[c * a.n_keep + keep] = cur;
+            if (a.sel) a.sel[c * a.n_keep + keep] = cur >= 0 ? cur : (a.carry_col >= 0 ? a.carry_col + c : -1);
             if (a.cnt) {
                 if (cur < 0)
                     ++carry;
@@ -691,6 +691,19 @@ __global__ __launch_bounds__(256) void gather_z_kernel(const ZT* __restrict__ Z,
         out[(size_t)q * d + i] = v;
 }
 
+// Chain states (caller layout, width OT) into columns col0 .. col0+nc-1 of the
+// coordinate-major proposal store, so kept-state selections are plain columns.
+template <typename OT, typename ZT>
+__global__ __launch_bounds__(256) void carry_cols_kernel(const OT* __restrict__ zs, int zs_coord_major,
+                                                         int64_t nc, int d, ZT* __restrict__ Z,
+                                                         int64_t ldz, int64_t col0) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    if (c >= nc) return;
+    const OT v = zs_coord_major ? zs[(size_t)i * nc + c] : zs[(size_t)c * d + i];
+    Z[(size_t)i * ldz + col0 + c] = (ZT)v;
+}
+
 // Copy rows of V (proposal lattice points, row-major [p][d]) selected by sel;
 // sel < 0 takes the carried state's row from vs (n_chains x d).
 __global__ __launch_bounds__(256) void gather_v_kernel(const double* __restrict__ V,
@@ -757,6 +770,7 @@ __global__ __launch_bounds__(256) void to_coord_major_kernel(const IT* __restric
 // |partial sums| < 2^53.
 template <typename ZT>
 __global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, int64_t ldz,
+                                                      const int64_t* __restrict__ sel,
                                                       const double* __restrict__ BT, int d,
                                                       int64_t n, double* __restrict__ V,
                                                       int64_t ldv, int64_t rb, int64_t rstride,
@@ -781,7 +795,7 @@ __global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, 
             const int kk = idx / BM, m = idx % BM;
             const int c = c0 + kk;
             const int64_t s = s0 + m;
-            As[kk][m] = (c < d && s < n) ? (double)Z[(size_t)c * ldz + s] : 0.0;
+            As[kk][m] = (c < d && s < n) ? (double)Z[(size_t)c * ldz + (sel ? sel[s] : s)] : 0.0;
             const int r = r0 + m;
             Bs[kk][m] = (c < d && r < d) ? BT[(size_t)c * d + r] : 0.0;
         }
@@ -836,6 +850,9 @@ typedef int v16i_t __attribute__((ext_vector_type(16)));
 
 template <typename ZT>
 __global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z, int64_t ldz,
+                                                    const int64_t* __restrict__ sel,
+                                                    const int* __restrict__ kchunk,
+                                                    const int* __restrict__ koff,
                                                     const int8_t* __restrict__ Bd1,
                                                     const int8_t* __restrict__ Bd0, int dc, int d,
                                                     int64_t n, double* __restrict__ V, int64_t ldv,
@@ -856,11 +873,15 @@ __global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z,
     }
     bool bad = false;
     const int zm = tid & 63, zq = tid >> 6;
-    for (int c0 = 0; c0 < d; c0 += KC) {
+    const int64_t zs_ = s0 + zm;
+    const int64_t zcol = zs_ < n ? (sel ? sel[zs_] : zs_) : 0;  // this thread's sample column
+    // only the K chunks where this row tile of B has a non-zero digit (exact skip)
+    const int ci0 = koff[blockIdx.x], ci1 = koff[blockIdx.x + 1];
+    for (int ci = ci0; ci < ci1; ++ci) {
+        const int c0 = kchunk[ci] * KC;
         {  // z chunk -> balanced base-256 digits, [sample][k] byte planes
-            const int64_t s = s0 + zm;
-            const bool sok = s < n;
-            const ZT* zp = Z + (size_t)(c0 + zq * 16) * ldz + (sok ? s : 0);
+            const bool sok = zs_ < n;
+            const ZT* zp = Z + (size_t)(c0 + zq * 16) * ldz + zcol;
             v4i_t w0, w1;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -1037,6 +1058,14 @@ hipError_t gather_z(const void* Z, int zb, int64_t ldz, const int64_t* sel, int6
     return hipGetLastError();
 }
 
+hipError_t carry_cols(const void* zs, int ob, int zs_coord_major, int64_t nc, int d, void* Z, int zb,
+                      int64_t ldz, int64_t col0, hipStream_t st) {
+    if (nc <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((nc + 255) / 256), (unsigned)d);
+    LGS_ZT(ob, OT, LGS_ZT(zb, ZT, hipLaunchKernelGGL((carry_cols_kernel<OT, ZT>), grid, dim3(256), 0, st, (const OT*)zs, zs_coord_major, nc, d, (ZT*)Z, ldz, col0)));
+    return hipGetLastError();
+}
+
 hipError_t gather_v(const double* V, const int64_t* sel, int64_t nq, int64_t q_per_chain,
                     const double* vs, int d, double* out, hipStream_t st) {
     if (nq <= 0) return hipSuccess;
@@ -1061,20 +1090,22 @@ hipError_t to_coord_major(const void* in, int ib, int64_t n, int d, void* Z, int
     return hipGetLastError();
 }
 
-hipError_t bz(const void* Z, int zb, int64_t ldz, const double* BT, int d, int64_t n, double* V,
-              int64_t ldv, int64_t rb, int64_t rstride, int64_t roff, hipStream_t st) {
+hipError_t bz(const void* Z, int zb, int64_t ldz, const int64_t* sel, const double* BT, int d,
+              int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
+              hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_gemm_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, BT, d, n, V, ldv, rb, rstride, roff));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_gemm_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, BT, d, n, V, ldv, rb, rstride, roff));
     return hipGetLastError();
 }
 
-hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int8_t* Bd1, const int8_t* Bd0, int dc,
-                 int d, int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
+hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const int* kchunk,
+                 const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
+                 double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((d + 127) / 128), (unsigned)((n + 63) / 64));
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags));
     return hipGetLastError();
 }
 
