@@ -95,6 +95,9 @@ struct lgs_ctx {
     bool has_B = false;
     DevBuf R, RP, RC, BT, coord;  // coord: cp | rii | sig | sig_ref | lterm | irii | ros | isr
     DevBuf CREC, RX;              // 32-row panels: per-coordinate records, coupling blocks
+    DevBuf RD, RDOFF;             // int8-digit far field: R digit fragments, panel offsets
+    bool has_rd = false, oz_off = false;  // oz_off: a |z| > 32767 was seen (sticky)
+    DevBuf H16, F0;               // int8-digit far field scratch: coefficient history, tile-0 sums
     DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
     DevBuf kchunk, koff;          // per 128-row tile of B: the 64-column chunks with a non-zero digit
     DevBuf etab;                  // SampleZ erf/exp table (lgs_device.h erf_gauss)
@@ -236,38 +239,61 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
     return a;
 }
 
-// Kernel choice: exact order on request; otherwise the MFMA far-field kernel when
-// the launch is whole waves with aligned coefficient rows, else the VALU panel
-// kernel.  LGS_KERNEL=valu|mfma|exact overrides.
-int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int zb, void* Z) {
+// Kernel choice: exact order on request; otherwise the MFMA kernel when the launch
+// is whole waves with aligned coefficient rows (32-row panels: int8-digit far field
+// unless disabled), else the VALU panel kernel.  LGS_KERNEL=valu|mfma|mfma64|exact
+// overrides (mfma64: fp64 MFMA far field).  Returns whether the int8-digit far
+// field was used.
+int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int zb, void* Z, bool& used_oz) {
     Scope s(c, 0);
     static const char* force = getenv("LGS_KERNEL");
     int kernel = lgs::kKernelValu;
+    used_oz = false;
     if (exact || (force && strcmp(force, "exact") == 0))
         kernel = lgs::kKernelExact;
     else if (!(force && strcmp(force, "valu") == 0) && a.n % 64 == 0 && a.ldz % 4 == 0 &&
              ((uintptr_t)Z % 16) == 0)
         kernel = lgs::kKernelMfma;
+    a.rd = nullptr;
+    if (kernel == lgs::kKernelMfma && c->panel == 32 && c->has_rd && !c->oz_off &&
+        !(force && strcmp(force, "mfma64") == 0)) {
+        const int shift = (int)((16 - c->d % 16) % 16);
+        const int64_t lanes = (a.n + 63) / 64 * 64;
+        const int64_t blocks = (c->d + shift) / 16 + 5;  // + one 64-column chunk of padding
+        int rc = c->H16.reserve((size_t)blocks * lanes * 32);
+        if (rc) return rc;
+        a.rd = c->RD.as<int8_t>();
+        a.rd_off = c->RDOFF.as<int64_t>();
+        a.h16 = c->H16.as<int16_t>();
+        a.h16_shift = shift;
+        a.h16_lanes = lanes;
+        used_oz = true;
+    }
     HIP_TRY(lgs::launch::klein(a, c->R.as<double>(), c->RP.as<double>(), c->RC.as<double>(),
                                c->panel, kernel, wl, zb, Z, c->stream));
     return LGS_OK;
 }
 
-// Klein launch into an internal coefficient store of width zb.  A 16-bit store
-// that overflowed (|z| > 32767) is redone at 32 bits -- same counters, same
-// samples -- and the context stays at 32 bits from then on.
+// Klein launch into an internal coefficient store of width zb.  A coefficient
+// beyond int16 (a 16-bit store, or the int16 history of the int8-digit far field)
+// redoes the launch -- same counters, same samples -- at 32 bits / with the fp64
+// far field, and the context keeps that choice.
 int run_klein_store(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int& zb, void* Z) {
-    int rc = run_klein(c, a, exact, wl, zb, Z);
-    if (rc || zb != 2) return rc;
+    bool oz = false;
+    int rc = run_klein(c, a, exact, wl, zb, Z, oz);
+    if (rc || (zb != 2 && !oz)) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     unsigned int f = 0;
     HIP_TRY(hipMemcpy(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost));
     if (!(f & lgs::kFlagOverflow16)) return LGS_OK;
     f &= ~lgs::kFlagOverflow16;
     HIP_TRY(hipMemcpy(c->flags.p, &f, sizeof(f), hipMemcpyHostToDevice));
-    c->zint = 4;
-    zb = 4;
-    return run_klein(c, a, exact, wl, zb, Z);
+    if (zb == 2) {
+        c->zint = 4;
+        zb = 4;
+    }
+    if (oz) c->oz_off = true;
+    return run_klein(c, a, exact, wl, zb, Z, oz);
 }
 
 int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
@@ -332,6 +358,11 @@ int lgs_create(lgs_ctx** out, int device) {
         if (v >= 64) c->max_props = v;
     }
     if (const char* m = getenv("LGS_SAMPLEZ_LIBM")) c->libm_samplez = atoi(m) != 0;
+    // far field of the 32-row-panel kernel: fp64 MFMA (default) or the exact int8-digit
+    // product (LGS_FAR=int8; correct, but its R-digit fragments serve 16 samples per
+    // load at the register budget of 3 waves/SIMD: 3.5x the L2 traffic, slower here)
+    c->oz_off = true;
+    if (const char* m = getenv("LGS_FAR")) c->oz_off = strcmp(m, "int8") != 0;
     {
         // {erf(j/64), exp(-(j/64)^2)}, j = 0..kErfTabLast, rounded from long double.
         std::vector<double> tab(2 * (lgs::kErfTabLast + 1));
@@ -461,6 +492,50 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
                     rxv[(size_t)pk * 256 + kk * 64 + l] = R[(size_t)row * dd + col];
             }
     }
+    // int8-digit far field (klein_mfma_kernel OZ): per 32-row panel, rows scaled by
+    // 2^E_i (|R_ij| 2^-E_i < 1/4 over the panel's far columns j >= p_hi) and split
+    // into 7 balanced base-256 digits (54 significant bits); the row's correction
+    // 128 * sum_j R~_ij (R~ = the digit approximation) is kept in long double.
+    const int64_t npan32 = (d + 31) / 32;
+    std::vector<double> rscale(dd, 1.0), rcorr(dd, 0.0);
+    std::vector<int64_t> rdoff(npan32 + 1, 0);
+    std::vector<int8_t> rdv;
+    bool oz = d <= lgs::kOzMaxD;
+    for (size_t k = 0; k < dd * dd && oz; ++k) oz = std::isfinite(R[k]);
+    if (oz) {
+        for (int64_t pk = 1; pk < npan32; ++pk)
+            rdoff[pk + 1] = rdoff[pk] + ((32 * pk + 63) / 64) * 2 * lgs::kOzDigits * 1024;
+        rdoff[1] = 0;
+        rdv.assign((size_t)std::max<int64_t>(rdoff[npan32], 16), 0);
+        for (int64_t pk = 1; pk < npan32; ++pk) {
+            const int64_t p_hi = d - 32 * pk, K = d - p_hi, nch = (K + 63) / 64;
+            int8_t* base = rdv.data() + rdoff[pk];
+            for (int r = 0; r < 32; ++r) {
+                const int64_t row = p_hi - 32 + r;
+                if (row < 0) continue;
+                double mx = 0.0;
+                for (int64_t j = p_hi; j < d; ++j) mx = std::max(mx, std::fabs(R[(size_t)row * dd + j]));
+                const int E = mx > 0.0 ? std::ilogb(mx) + 3 : 0;
+                rscale[row] = std::ldexp(1.0, E);
+                long double corr = 0.0L;
+                const int t = r >> 4, n = r & 15;
+                for (int64_t j = p_hi; j < d; ++j) {
+                    long long M = std::llrint(std::ldexp(R[(size_t)row * dd + j], 56 - E));
+                    corr += (long double)M;
+                    const int64_t kk = j - p_hi, ch = kk / 64, h = (kk % 64) / 16, e = kk % 16;
+                    for (int a = lgs::kOzDigits; a >= 1; --a) {  // least significant digit first
+                        const long long dg = ((M % 256) + 256 + 128) % 256 - 128;
+                        M = (M - dg) / 256;
+                        const int64_t lane = h * 16 + n;
+                        base[(((ch * 2 + t) * lgs::kOzDigits + (a - 1)) * 64 + lane) * 16 + e] = (int8_t)dg;
+                    }
+                    if (M != 0) return fail(LGS_ERR_INVALID, "R digit split overflow");
+                }
+                rcorr[row] = (double)(128.0L * std::ldexp(corr, E - 56));
+            }
+            (void)nch;
+        }
+    }
     // per-coordinate records (lgs_kernels.h kRec*)
     std::vector<double> crec(dd * lgs::kRecStride, 0.0);
     for (size_t i = 0; i < dd; ++i) {
@@ -472,6 +547,14 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
         r[lgs::kRecIsr] = co[7 * dd + i];
         r[lgs::kRecLterm] = co[4 * dd + i];
         std::copy(rsv.data() + i * 15, rsv.data() + i * 15 + 15, r + lgs::kRecRs);
+        r[lgs::kRecScale] = rscale[i];
+        r[lgs::kRecCorr] = rcorr[i];
+    }
+    c->has_rd = oz;
+    if (oz) {
+        if ((rc = c->RD.reserve(rdv.size())) || (rc = c->RDOFF.reserve(rdoff.size() * 8))) return rc;
+        HIP_TRY(hipMemcpy(c->RD.p, rdv.data(), rdv.size(), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->RDOFF.p, rdoff.data(), rdoff.size() * 8, hipMemcpyHostToDevice));
     }
     if ((rc = c->CREC.reserve(crec.size() * 8)) || (rc = c->RX.reserve(rxv.size() * 8))) return rc;
     HIP_TRY(hipMemcpy(c->CREC.p, crec.data(), crec.size() * 8, hipMemcpyHostToDevice));

@@ -31,7 +31,14 @@ constexpr int kSzcStride = 24;
 // Staged into LDS once per 32-row panel by klein_mfma_kernel.
 constexpr int kRecCp = kSzUsed, kRecIrii = kSzUsed + 1, kRecRos = kSzUsed + 2,
               kRecIsr = kSzUsed + 3, kRecLterm = kSzUsed + 4, kRecRs = kSzUsed + 5;
-constexpr int kRecStride = kRecRs + 16;  // 42 (one pad): 336 bytes, 16-byte multiple
+// int8-digit far field (klein_mfma_kernel OZ): row scale 2^E_i and the offset
+// correction 128 * sum_j R~_ij of the coordinate's row over its panel's far columns
+constexpr int kRecScale = kRecRs + 15, kRecCorr = kRecRs + 16;
+constexpr int kRecStride = kRecRs + 18;  // 44: 352 bytes, 16-byte multiple
+// int8-digit far field layout: per 32-row panel pk >= 1 (K = 32 pk far columns,
+// ceil(K/64) chunks of 64): [chunk][row tile t][digit a][lane][16 bytes]
+constexpr int kOzDigits = 7;
+constexpr int kOzMaxD = 32768;  // int32 class sums stay exact: 2 * K * 2^14 < 2^31
 constexpr int kSzRound = 0;    // sigma_i < 1e-10: round(mu), no draw
 constexpr int kSzSmall = 1;    // sigma_i < 4: <= 4-point exponent path / table walk
 constexpr int kSzClosed = 2;   // uncapped window of +-rf*sigma, rf >= 9: S = 2 sc, base = -sc
@@ -77,6 +84,12 @@ struct KleinArgs {
     const double* etab;  // SampleZ erf/exp table (nullptr: ocml libm path)
     const double* szc;   // per-coordinate SampleZ constants (nullptr: generic sample_z)
     const double* crec;  // per-coordinate records (kRecStride doubles, layout above)
+    // int8-digit far field (nullptr rd: fp64 MFMA far field)
+    const int8_t* rd;        // R digit fragments, all panels
+    const int64_t* rd_off;   // byte offset of panel pk in rd
+    int16_t* h16;            // coefficient history, [(i + h16_shift)/16][lane][16] int16
+    int h16_shift;           // (16 - d % 16) % 16
+    int64_t h16_lanes;       // lanes per 16-coordinate block (>= n)
     const double* rx;    // per 32-row panel: 16x16 block R[p_hi-32.., p_hi-16..] as MFMA A fragments
 };
 

@@ -286,10 +286,109 @@ struct ZQuad<int64_t> {
     __device__ __forceinline__ double get(int g) const { return (double)v[g]; }
 };
 
-template <typename ZT, int PB, bool WL>
+// ---------------------------------------------------- int8-digit far field
+// F_i = sum_{j >= p_hi} R_ij x_j for the 32 rows of panel pk and the wave's 64
+// samples, exactly enough to stand in for fp64: rows scaled by 2^E_i and split
+// into 7 balanced base-256 digits r_a (|R 2^-E| < 1/4, 54 significant bits,
+// host: lgs_set_basis); coefficients x in [-32767, 32767] from the int16 history,
+// x = 256 x1 + x0 + 128 with x1 = the high byte and x0 = low byte ^ 0x80 (both
+// signed), so a digit plane is two byte permutes of the raw int16 pairs.  Class
+// c = a - b of r_a x_b (weight 256^-c) is summed exactly in int32 on
+// v_mfma_i32_16x16x64_i8 (|sum| <= 2 K 2^14 < 2^31 for d <= 32768); then
+// F_i = 2^E_i sum_c 256^-c C_c + 128 sum_j R~_ij (host-precomputed).
+// Four passes (16 samples each) keep 2 row tiles x 8 classes = 64 accumulator
+// VGPRs.  Row tile 1 (the upper sub-panel) goes to acc through the LDS tile;
+// tile 0 is parked in the per-wave scratch f0 and moved into the LDS tile once
+// the upper rows are loaded (the LDS tile is free during the upper sub-panel).
+typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_hi, int64_t p0, int lane,
+                                             lds_cdptr rec, double* F, int LDF, double (&acc)[16]) {
+    const int d = a.d;
+    const int K = d - p_hi, nch = (K + 63) / 64;
+    const int h = lane >> 4, n = lane & 15;
+    const int8_t* __restrict__ rbase =
+        a.rd + ((const __attribute__((address_space(4))) int64_t*)a.rd_off)[pk];
+    const size_t blk0 = (size_t)((p_hi + a.h16_shift) >> 4) + h;
+    const size_t hstep = (size_t)4 * a.h16_lanes * 16;  // 4 history blocks = one 64-column chunk
+    double t0v[4][4];  // lower row tile, D layout, until the LDS tile is free
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) t0v[g][reg] = 0.0;
+#pragma unroll 1
+    for (int g = 0; g < 4; ++g) {
+        v4i32_t cc[2][8];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) cc[t][c] = (v4i32_t){0, 0, 0, 0};
+        const int16_t* __restrict__ hp = a.h16 + (blk0 * a.h16_lanes + p0 + 16 * g + n) * 16;
+        const v4i32_t* __restrict__ ap = (const v4i32_t*)rbase + lane;
+#pragma unroll 1
+        for (int c = 0; c < nch; ++c) {
+            const v4u_t w0 = __builtin_nontemporal_load((const v4u_t*)hp);
+            const v4u_t w1 = __builtin_nontemporal_load((const v4u_t*)hp + 1);
+            v4i32_t xh, xl;
+            xh[0] = (int)__builtin_amdgcn_perm(w0[1], w0[0], 0x07050301u);
+            xh[1] = (int)__builtin_amdgcn_perm(w0[3], w0[2], 0x07050301u);
+            xh[2] = (int)__builtin_amdgcn_perm(w1[1], w1[0], 0x07050301u);
+            xh[3] = (int)__builtin_amdgcn_perm(w1[3], w1[2], 0x07050301u);
+            xl[0] = (int)(__builtin_amdgcn_perm(w0[1], w0[0], 0x06040200u) ^ 0x80808080u);
+            xl[1] = (int)(__builtin_amdgcn_perm(w0[3], w0[2], 0x06040200u) ^ 0x80808080u);
+            xl[2] = (int)(__builtin_amdgcn_perm(w1[1], w1[0], 0x06040200u) ^ 0x80808080u);
+            xl[3] = (int)(__builtin_amdgcn_perm(w1[3], w1[2], 0x06040200u) ^ 0x80808080u);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+#pragma unroll
+                for (int dg = 0; dg < kOzDigits; ++dg) {
+                    const v4i32_t av = ap[(t * kOzDigits + dg) * 64];
+                    // digit a = dg + 1: class a - 1 with the high x digit, class a with the low
+                    cc[t][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xh, cc[t][dg], 0, 0, 0);
+                    cc[t][dg + 1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xl, cc[t][dg + 1], 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);  // bound the operand loads in flight
+            }
+            hp += hstep;
+            ap += 2 * kOzDigits * 64;
+        }
+        // classes -> fp64; D layout: rows 4h + reg of the tile, sample 16g + n
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int row = 16 * t + 4 * h + reg;  // panel row = record index
+                double sv = (double)cc[t][7][reg];
+#pragma unroll
+                for (int c = 6; c >= 0; --c) sv = fma(sv, 0.00390625, (double)cc[t][c][reg]);
+                const lds_cdptr rr = rec + row * kRecStride;
+                const double fv = fma(sv, rr[kRecScale], rr[kRecCorr]);
+                if (t == 1) {
+                    F[(4 * h + reg) * LDF + 16 * g + n] = fv;
+                } else {
+#pragma unroll
+                    for (int gg = 0; gg < 4; ++gg) t0v[gg][reg] = g == gg ? fv : t0v[gg][reg];
+                }
+            }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = F[r * LDF + lane];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) F[(4 * h + reg) * LDF + 16 * g + n] = t0v[g][reg];
+}
+
 #ifndef LGS_MFMA_LB32
 #define LGS_MFMA_LB32 3
 #endif
+// OZ (32-row panels only): far field as an exact int8-digit product on
+// v_mfma_i32_16x16x64_i8 instead of fp64 MFMA (see oz_far_field).
+template <typename ZT, int PB, bool WL, bool OZ = false>
 __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_kernel(const KleinArgs a,
                                                             const double* __restrict__ RP,
                                                             const double* __restrict__ RC,
@@ -341,6 +440,10 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
             // stored by this wave's lanes in earlier panels
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
+          if constexpr (OZ && PB == 32) {
+            oz_far_field(a, pk, p_hi, p0, lane, (lds_cdptr)rec_lds, F, LDF, acc);
+            (void)NT;
+          } else {
             d4_t f[NT][4];
 #pragma unroll
             for (int t = 0; t < NT; ++t)
@@ -423,6 +526,7 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
                     __builtin_amdgcn_wave_barrier();
                 }
             }
+          }
         } else {
 #pragma unroll
             for (int r = 0; r < NACC; ++r) acc[r] = 0.0;
@@ -443,6 +547,12 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
                     const double mu = (rec[kRecCp] - acc[15]) * rec[kRecIrii];
                     const double zi = decide_coord_rec<WL>(a, i, mu, rec, rs, lw, flags, etab_s);
                     store_z(Z, (size_t)i * ldz + p, zi, flags);
+                    if constexpr (OZ) {  // int16 history for the int8-digit far field
+                        const int ih = i + a.h16_shift;
+                        if (!(zi <= 32767.0 && zi >= -32767.0)) flags |= kFlagOverflow16;
+                        a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] =
+                            (int16_t)fmin(fmax(zi, -32767.0), 32767.0);
+                    }
                     const lds_cdptr rc = rec + kRecRs;
 #pragma unroll
                     for (int k = 0; k < 15; ++k) acc[k] = fma(rc[14 - k], zi, acc[k]);
@@ -978,7 +1088,12 @@ template <typename ZT, int PB>
 static void klein_pb(const KleinArgs& a, const double* RP, const double* RC, int kernel, bool wl,
                      ZT* z, dim3 grid, hipStream_t st) {
     if (kernel == kKernelMfma) {
-        if (wl)
+        if (PB == 32 && a.rd) {  // int8-digit far field
+            if (wl)
+                hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, true, true>), grid, dim3(256), 0, st, a, RP, RC, z);
+            else
+                hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, false, true>), grid, dim3(256), 0, st, a, RP, RC, z);
+        } else if (wl)
             hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, true>), grid, dim3(256), 0, st, a, RP, RC, z);
         else
             hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, false>), grid, dim3(256), 0, st, a, RP, RC, z);

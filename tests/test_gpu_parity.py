@@ -108,6 +108,54 @@ def test_klein_coord_constants_vs_generic_samplez(ctx, ctx_libm, oracle, capi, p
     assert np.array_equal(out[0]["z"][:200], o["z"])
 
 
+@pytest.fixture(scope="module")
+def ctx_far8(capi):
+    """A context whose 32-row-panel kernel uses the int8-digit far field."""
+    os.environ["LGS_FAR"] = "int8"
+    try:
+        return capi.Context(0)
+    finally:
+        del os.environ["LGS_FAR"]
+
+
+def test_int8_digit_far_field_matches_fp64_far_field(ctx, ctx_far8, oracle):
+    """The exact int8-digit far field and the fp64 MFMA far field give the same
+    coefficients on the full-size NTRU basis, and both match the oracle."""
+    from lgs_amd.lattices import build_config
+    lat, sigma = build_config("C3_ntru512")
+    B = lat.basis
+    R = np.linalg.qr(B)[1]
+    R = np.ascontiguousarray(R * np.where(np.diag(R) < 0, -1.0, 1.0)[:, None])
+    cp = np.zeros(B.shape[0])
+    out = []
+    for c in (ctx_far8, ctx):
+        c.set_basis(R, cp, B, sigma)
+        out.append(c.klein_host(7, 1 << 20, 4096, want_z=True, want_v=False)["z"])
+    assert np.array_equal(out[0], out[1])
+    o = oracle.klein(R, cp, sigma, 64, seed=7, first_sample=1 << 20)
+    assert np.array_equal(out[0][:64], o["z"])
+
+
+def test_int8_digit_far_field_overflow_falls_back(capi, oracle):
+    """|z| > 32767 cannot use the int16 history: the launch is redone with the fp64
+    far field (same counters) and the context keeps it."""
+    rng = np.random.default_rng(5)
+    d = 96
+    R = np.triu(rng.normal(size=(d, d)) * 0.01, 1)
+    R[np.diag_indices(d)] = rng.uniform(0.5, 2.0, d)
+    cp = rng.normal(size=d) * 4e4
+    os.environ["LGS_FAR"] = "int8"
+    try:
+        c = capi.Context(0)
+    finally:
+        del os.environ["LGS_FAR"]
+    c.set_basis(R, cp, None, 3.0)
+    r = c.klein_host(11, 0, 256, want_z=True, want_v=False)
+    o = oracle.klein(R, cp, 3.0, 256, seed=11, first_sample=0)
+    assert np.abs(o["z"]).max() > 32767
+    assert np.array_equal(r["z"], o["z"])
+
+
 def test_klein_full_size_ntru1024_vs_oracle(ctx, oracle):
     """BASELINE config C3 basis (d = 1024): device vs oracle on 64 samples, both kernels."""
     from lgs_amd.lattices import build_config
