@@ -255,7 +255,8 @@ int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int zb, void* 
              ((uintptr_t)Z % 16) == 0)
         kernel = lgs::kKernelMfma;
     a.rd = nullptr;
-    if (kernel == lgs::kKernelMfma && c->panel == 32 && c->has_rd && !c->oz_off &&
+    // (the int8-digit far field synchronises the block per step: whole blocks only)
+    if (kernel == lgs::kKernelMfma && c->panel == 32 && c->has_rd && !c->oz_off && a.n % 256 == 0 &&
         !(force && strcmp(force, "mfma64") == 0)) {
         const int shift = (int)((16 - c->d % 16) % 16);
         const int64_t lanes = (a.n + 63) / 64 * 64;
@@ -358,11 +359,9 @@ int lgs_create(lgs_ctx** out, int device) {
         if (v >= 64) c->max_props = v;
     }
     if (const char* m = getenv("LGS_SAMPLEZ_LIBM")) c->libm_samplez = atoi(m) != 0;
-    // far field of the 32-row-panel kernel: fp64 MFMA (default) or the exact int8-digit
-    // product (LGS_FAR=int8; correct, but its R-digit fragments serve 16 samples per
-    // load at the register budget of 3 waves/SIMD: 3.5x the L2 traffic, slower here)
-    c->oz_off = true;
-    if (const char* m = getenv("LGS_FAR")) c->oz_off = strcmp(m, "int8") != 0;
+    // far field of the 32-row-panel kernel: the exact int8-digit product (default)
+    // or fp64 MFMA (LGS_FAR=fp64)
+    if (const char* m = getenv("LGS_FAR")) c->oz_off = strcmp(m, "fp64") == 0;
     {
         // {erf(j/64), exp(-(j/64)^2)}, j = 0..kErfTabLast, rounded from long double.
         std::vector<double> tab(2 * (lgs::kErfTabLast + 1));

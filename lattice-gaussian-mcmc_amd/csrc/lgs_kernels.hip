@@ -17,6 +17,8 @@
 //
 // Compiled with -ffp-contract=off (see lgs_device.h).
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <stdint.h>
 
 #include "lgs_device.h"
@@ -303,12 +305,17 @@ struct ZQuad<int64_t> {
 typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_hi, int64_t p0, int lane,
-                                             lds_cdptr rec, double* F, int LDF, double (&acc)[16]) {
+                                             lds_cdptr rec, double* F, int LDF, double (&acc)[16],
+                                             int8_t* ash) {
     const int d = a.d;
     const int K = d - p_hi, nch = (K + 63) / 64;
-    const int h = lane >> 4, n = lane & 15;
-    const int8_t* __restrict__ rbase =
-        a.rd + ((const __attribute__((address_space(4))) int64_t*)a.rd_off)[pk];
+    const int h = lane >> 4, n = lane & 15, tid = threadIdx.x;
+    // block-shared R-digit slab of one 64-column chunk (both row tiles): 896 x 16 B,
+    // double-buffered in LDS; thread tid stages pieces tid + 256 m (m < 4, < 896)
+    constexpr int SLAB = 2 * kOzDigits * 64;
+    const v4i32_t* __restrict__ rsrc =
+        (const v4i32_t*)(a.rd + ((const __attribute__((address_space(4))) int64_t*)a.rd_off)[pk]);
+    v4i32_t* ash4 = (v4i32_t*)ash;
     const size_t blk0 = (size_t)((p_hi + a.h16_shift) >> 4) + h;
     const size_t hstep = (size_t)4 * a.h16_lanes * 16;  // 4 history blocks = one 64-column chunk
     double t0v[4][4];  // lower row tile, D layout, until the LDS tile is free
@@ -316,60 +323,102 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
     for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) t0v[g][reg] = 0.0;
+    auto slab_load = [&](int ch, v4i32_t (&pf)[4]) {
+        const v4i32_t* src = rsrc + (size_t)ch * SLAB;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if (tid + 256 * m < SLAB) pf[m] = src[tid + 256 * m];
+    };
+    auto slab_store = [&](int buf, const v4i32_t (&pf)[4]) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if (tid + 256 * m < SLAB) ash4[buf * SLAB + tid + 256 * m] = pf[m];
+    };
+    // two passes of two 16-sample groups: each A fragment read from LDS feeds 4 MFMAs
 #pragma unroll 1
-    for (int g = 0; g < 4; ++g) {
-        v4i32_t cc[2][8];
+    for (int gp = 0; gp < 2; ++gp) {
+        v4i32_t cc[2][2][8];  // [group][row tile][class]
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int q = 0; q < 2; ++q)
 #pragma unroll
-            for (int c = 0; c < 8; ++c) cc[t][c] = (v4i32_t){0, 0, 0, 0};
-        const int16_t* __restrict__ hp = a.h16 + (blk0 * a.h16_lanes + p0 + 16 * g + n) * 16;
-        const v4i32_t* __restrict__ ap = (const v4i32_t*)rbase + lane;
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int c = 0; c < 8; ++c) cc[q][t][c] = (v4i32_t){0, 0, 0, 0};
+        const int16_t* __restrict__ hp0 = a.h16 + (blk0 * a.h16_lanes + p0 + 32 * gp + n) * 16;
+        const int16_t* __restrict__ hp1 = hp0 + 16 * 16;  // group 2gp + 1: 16 lanes further
+        v4i32_t pf[4];
+        __syncthreads();  // previous pass done with both buffers
+        slab_load(0, pf);
+        slab_store(0, pf);
+        if (nch > 1) slab_load(1, pf);
+        v4u_t w[2][2];
+        w[0][0] = __builtin_nontemporal_load((const v4u_t*)hp0);
+        w[0][1] = __builtin_nontemporal_load((const v4u_t*)hp0 + 1);
+        w[1][0] = __builtin_nontemporal_load((const v4u_t*)hp1);
+        w[1][1] = __builtin_nontemporal_load((const v4u_t*)hp1 + 1);
+        __syncthreads();
 #pragma unroll 1
-        for (int c = 0; c < nch; ++c) {
-            const v4u_t w0 = __builtin_nontemporal_load((const v4u_t*)hp);
-            const v4u_t w1 = __builtin_nontemporal_load((const v4u_t*)hp + 1);
-            v4i32_t xh, xl;
-            xh[0] = (int)__builtin_amdgcn_perm(w0[1], w0[0], 0x07050301u);
-            xh[1] = (int)__builtin_amdgcn_perm(w0[3], w0[2], 0x07050301u);
-            xh[2] = (int)__builtin_amdgcn_perm(w1[1], w1[0], 0x07050301u);
-            xh[3] = (int)__builtin_amdgcn_perm(w1[3], w1[2], 0x07050301u);
-            xl[0] = (int)(__builtin_amdgcn_perm(w0[1], w0[0], 0x06040200u) ^ 0x80808080u);
-            xl[1] = (int)(__builtin_amdgcn_perm(w0[3], w0[2], 0x06040200u) ^ 0x80808080u);
-            xl[2] = (int)(__builtin_amdgcn_perm(w1[1], w1[0], 0x06040200u) ^ 0x80808080u);
-            xl[3] = (int)(__builtin_amdgcn_perm(w1[3], w1[2], 0x06040200u) ^ 0x80808080u);
+        for (int ch = 0; ch < nch; ++ch) {
+            v4i32_t xh[2], xl[2];  // history of chunk ch -> digit planes, per group
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
+            for (int q = 0; q < 2; ++q) {
+                const v4u_t w0 = w[q][0], w1 = w[q][1];
+                xh[q][0] = (int)__builtin_amdgcn_perm(w0[1], w0[0], 0x07050301u);
+                xh[q][1] = (int)__builtin_amdgcn_perm(w0[3], w0[2], 0x07050301u);
+                xh[q][2] = (int)__builtin_amdgcn_perm(w1[1], w1[0], 0x07050301u);
+                xh[q][3] = (int)__builtin_amdgcn_perm(w1[3], w1[2], 0x07050301u);
+                xl[q][0] = (int)(__builtin_amdgcn_perm(w0[1], w0[0], 0x06040200u) ^ 0x80808080u);
+                xl[q][1] = (int)(__builtin_amdgcn_perm(w0[3], w0[2], 0x06040200u) ^ 0x80808080u);
+                xl[q][2] = (int)(__builtin_amdgcn_perm(w1[1], w1[0], 0x06040200u) ^ 0x80808080u);
+                xl[q][3] = (int)(__builtin_amdgcn_perm(w1[3], w1[2], 0x06040200u) ^ 0x80808080u);
+            }
+            if (ch + 1 < nch) {  // history of the next chunk; slab ch+1 -> LDS, fetch slab ch+2
+                hp0 += hstep;
+                hp1 += hstep;
+                w[0][0] = __builtin_nontemporal_load((const v4u_t*)hp0);
+                w[0][1] = __builtin_nontemporal_load((const v4u_t*)hp0 + 1);
+                w[1][0] = __builtin_nontemporal_load((const v4u_t*)hp1);
+                w[1][1] = __builtin_nontemporal_load((const v4u_t*)hp1 + 1);
+                slab_store((ch + 1) & 1, pf);
+                if (ch + 2 < nch) slab_load(ch + 2, pf);
+            }
+            const v4i32_t* sl = ash4 + (ch & 1) * SLAB + lane;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int dg = 0; dg < kOzDigits; ++dg) {
-                    const v4i32_t av = ap[(t * kOzDigits + dg) * 64];
+                    const v4i32_t av = sl[(t * kOzDigits + dg) * 64];
                     // digit a = dg + 1: class a - 1 with the high x digit, class a with the low
-                    cc[t][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xh, cc[t][dg], 0, 0, 0);
-                    cc[t][dg + 1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xl, cc[t][dg + 1], 0, 0, 0);
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        cc[q][t][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xh[q], cc[q][t][dg], 0, 0, 0);
+                        cc[q][t][dg + 1] =
+                            __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xl[q], cc[q][t][dg + 1], 0, 0, 0);
+                    }
                 }
-                __builtin_amdgcn_sched_barrier(0);  // bound the operand loads in flight
-            }
-            hp += hstep;
-            ap += 2 * kOzDigits * 64;
+            __syncthreads();  // slab ch+1 complete; slab ch reads done before it is reused
         }
         // classes -> fp64; D layout: rows 4h + reg of the tile, sample 16g + n
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int q = 0; q < 2; ++q)
 #pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                const int row = 16 * t + 4 * h + reg;  // panel row = record index
-                double sv = (double)cc[t][7][reg];
+            for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int c = 6; c >= 0; --c) sv = fma(sv, 0.00390625, (double)cc[t][c][reg]);
-                const lds_cdptr rr = rec + row * kRecStride;
-                const double fv = fma(sv, rr[kRecScale], rr[kRecCorr]);
-                if (t == 1) {
-                    F[(4 * h + reg) * LDF + 16 * g + n] = fv;
-                } else {
+                for (int reg = 0; reg < 4; ++reg) {
+                    const int g = 2 * gp + q;
+                    const int row = 16 * t + 4 * h + reg;  // panel row = record index
+                    double sv = (double)cc[q][t][7][reg];
 #pragma unroll
-                    for (int gg = 0; gg < 4; ++gg) t0v[gg][reg] = g == gg ? fv : t0v[gg][reg];
+                    for (int c = 6; c >= 0; --c) sv = fma(sv, 0.00390625, (double)cc[q][t][c][reg]);
+                    const lds_cdptr rr = rec + row * kRecStride;
+                    const double fv = fma(sv, rr[kRecScale], rr[kRecCorr]);
+                    if (t == 1) {
+                        F[(4 * h + reg) * LDF + 16 * g + n] = fv;
+                    } else {
+#pragma unroll
+                        for (int gg = 0; gg < 4; ++gg) t0v[gg][reg] = g == gg ? fv : t0v[gg][reg];
+                    }
                 }
-            }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -389,14 +438,22 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
 // OZ (32-row panels only): far field as an exact int8-digit product on
 // v_mfma_i32_16x16x64_i8 instead of fp64 MFMA (see oz_far_field).
 template <typename ZT, int PB, bool WL, bool OZ = false>
-__global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_kernel(const KleinArgs a,
+__global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void klein_mfma_kernel(const KleinArgs a,
                                                             const double* __restrict__ RP,
                                                             const double* __restrict__ RC,
                                                             ZT* __restrict__ Z) {
     constexpr int NT = PB / 16, LDF = 65;  // LDS tile pitch (doubles): conflict-free row reads
     __shared__ double Fl[4][16 * LDF];
-    __shared__ double tab_lds[2 * (kErfTabLast + 1)];
-    const lds_cdptr etab_s = stage_etab(tab_lds, a.etab);
+    // OZ: the erf table stays in global memory (L1-resident lookups measured as fast
+    // as LDS) to leave LDS for the block-shared R-digit slab of the far field
+    __shared__ double tab_lds[OZ ? 2 : 2 * (kErfTabLast + 1)];
+    __shared__ __attribute__((aligned(16))) int8_t ash[OZ ? 2 * 2 * kOzDigits * 1024 : 16];  // 2 x 14 KB
+    using ETP = std::conditional_t<OZ, const double*, lds_cdptr>;
+    ETP etab_s;
+    if constexpr (OZ)
+        etab_s = a.etab;
+    else
+        etab_s = stage_etab(tab_lds, a.etab);
     // 32-row panels: the panel's per-coordinate records, staged block-wide
     __shared__ double rec_lds[PB == 32 ? 32 * kRecStride : 2];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -441,7 +498,7 @@ __global__ __launch_bounds__(256, PB == 32 ? LGS_MFMA_LB32 : 3) void klein_mfma_
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
           if constexpr (OZ && PB == 32) {
-            oz_far_field(a, pk, p_hi, p0, lane, (lds_cdptr)rec_lds, F, LDF, acc);
+            oz_far_field(a, pk, p_hi, p0, lane, (lds_cdptr)rec_lds, F, LDF, acc, ash);
             (void)NT;
           } else {
             d4_t f[NT][4];

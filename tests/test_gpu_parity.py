@@ -109,16 +109,16 @@ def test_klein_coord_constants_vs_generic_samplez(ctx, ctx_libm, oracle, capi, p
 
 
 @pytest.fixture(scope="module")
-def ctx_far8(capi):
-    """A context whose 32-row-panel kernel uses the int8-digit far field."""
-    os.environ["LGS_FAR"] = "int8"
+def ctx_far64(capi):
+    """A context whose 32-row-panel kernel uses the fp64 MFMA far field."""
+    os.environ["LGS_FAR"] = "fp64"
     try:
         return capi.Context(0)
     finally:
         del os.environ["LGS_FAR"]
 
 
-def test_int8_digit_far_field_matches_fp64_far_field(ctx, ctx_far8, oracle):
+def test_int8_digit_far_field_matches_fp64_far_field(ctx, ctx_far64, oracle):
     """The exact int8-digit far field and the fp64 MFMA far field give the same
     coefficients on the full-size NTRU basis, and both match the oracle."""
     from lgs_amd.lattices import build_config
@@ -128,7 +128,7 @@ def test_int8_digit_far_field_matches_fp64_far_field(ctx, ctx_far8, oracle):
     R = np.ascontiguousarray(R * np.where(np.diag(R) < 0, -1.0, 1.0)[:, None])
     cp = np.zeros(B.shape[0])
     out = []
-    for c in (ctx_far8, ctx):
+    for c in (ctx, ctx_far64):
         c.set_basis(R, cp, B, sigma)
         out.append(c.klein_host(7, 1 << 20, 4096, want_z=True, want_v=False)["z"])
     assert np.array_equal(out[0], out[1])
@@ -144,11 +144,7 @@ def test_int8_digit_far_field_overflow_falls_back(capi, oracle):
     R = np.triu(rng.normal(size=(d, d)) * 0.01, 1)
     R[np.diag_indices(d)] = rng.uniform(0.5, 2.0, d)
     cp = rng.normal(size=d) * 4e4
-    os.environ["LGS_FAR"] = "int8"
-    try:
-        c = capi.Context(0)
-    finally:
-        del os.environ["LGS_FAR"]
+    c = capi.Context(0)
     c.set_basis(R, cp, None, 3.0)
     r = c.klein_host(11, 0, 256, want_z=True, want_v=False)
     o = oracle.klein(R, cp, 3.0, 256, seed=11, first_sample=0)
