@@ -101,6 +101,7 @@ struct lgs_ctx {
     DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
     DevBuf kchunk, koff;          // per 128-row tile of B: the 64-column chunks with a non-zero digit
     DevBuf etab;                  // SampleZ erf/exp table (lgs_device.h erf_gauss)
+    DevBuf etab2;                 // its Taylor-coefficient form (lgs_device.h CoefTab)
     DevBuf szc;                   // per-coordinate SampleZ constants (lgs_kernels.h kSzc*)
     bool libm_samplez = false;    // LGS_SAMPLEZ_LIBM=1: ocml erf/exp/erfinv path instead
     bool has_Bi8 = false;
@@ -233,6 +234,7 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
     a.seed = seed;
     a.flags = c->flags.as<unsigned int>();
     a.etab = c->libm_samplez ? nullptr : c->etab.as<double>();
+    a.etab2 = c->etab2.as<double>();
     a.szc = c->libm_samplez ? nullptr : c->szc.as<double>();
     a.crec = c->CREC.as<double>();
     a.rx = c->RX.as<double>();
@@ -374,6 +376,38 @@ int lgs_create(lgs_ctx** out, int device) {
         if (!rc) {
             e = hipMemcpy(c->etab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice);
             if (e != hipSuccess) rc = fail(LGS_ERR_HIP, "etab upload: %s", hipGetErrorString(e));
+        }
+        if (rc) {
+            (void)hipStreamDestroy(c->own);
+            delete c;
+            return rc;
+        }
+        // Taylor coefficients per grid point (lgs_device.h CoefTab), long double
+        std::vector<double> t2((size_t)(lgs::kErfTabLast + 1) * lgs::kCoefStride, 0.0);
+        const long double two_over_sqrtpi = 1.128379167095512573896158903121545172L;
+        for (int j = 0; j <= lgs::kErfTabLast; ++j) {
+            const long double y0 = (long double)j / 64.0L, G = expl(-y0 * y0);
+            long double H[10];
+            H[0] = 1.0L;
+            H[1] = 2.0L * y0;
+            for (int m = 1; m < 9; ++m) H[m + 1] = 2.0L * y0 * H[m] - 2.0L * m * H[m - 1];
+            double* r = t2.data() + (size_t)j * lgs::kCoefStride;
+            r[0] = (double)erfl(y0);
+            long double fact = 1.0L;
+            for (int m = 1; m <= 7; ++m) {
+                fact *= m;
+                r[m] = (double)(two_over_sqrtpi * ((m - 1) % 2 ? -1.0L : 1.0L) * H[m - 1] * G / fact);
+            }
+            fact = 1.0L;
+            for (int m = 0; m <= 8; ++m) {
+                if (m) fact *= m;
+                r[8 + m] = (double)((m % 2 ? -1.0L : 1.0L) * H[m] * G / fact);
+            }
+        }
+        rc = c->etab2.reserve(t2.size() * 8);
+        if (!rc) {
+            e = hipMemcpy(c->etab2.p, t2.data(), t2.size() * 8, hipMemcpyHostToDevice);
+            if (e != hipSuccess) rc = fail(LGS_ERR_HIP, "etab2 upload: %s", hipGetErrorString(e));
         }
         if (rc) {
             (void)hipStreamDestroy(c->own);

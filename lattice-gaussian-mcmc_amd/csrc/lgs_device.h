@@ -38,10 +38,18 @@ __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
         }
+#ifndef LGS_PHILOX_MULHI
+        // one 32x32->64 multiply (v_mad_u64_u32) per product instead of mul_lo + mul_hi
+        const uint64_t m0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t m1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t lo0 = (uint32_t)m0, hi0 = (uint32_t)(m0 >> 32);
+        const uint32_t lo1 = (uint32_t)m1, hi1 = (uint32_t)(m1 >> 32);
+#else
         const uint32_t lo0 = 0xD2511F53u * c0;
         const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
         const uint32_t lo1 = 0xCD9E8D57u * c2;
         const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
+#endif
         const uint32_t n0 = hi1 ^ c1 ^ k0;
         const uint32_t n2 = hi0 ^ c3 ^ k1;
         c0 = n0;
@@ -254,6 +262,47 @@ __device__ __forceinline__ ErfExp erf_gauss(double y, TP etab) {
     ErfExp r;
     r.erf = copysign(big ? 1.0 : e, y);
     r.g = big ? 0.0 : G * p;
+    return r;
+}
+
+// Coefficient form of the same table (used by the 32-row-panel Klein kernel):
+// per grid point y0 = j/64, 18 doubles: the Taylor coefficients in h = y - y0 of
+// erf (a0 = erf(y0), a_n = 2/sqrt(pi) (-1)^(n-1) H_{n-1}(y0) e^{-y0^2}/n!, n <= 7)
+// and of e^{-y^2} (b_n = (-1)^n H_n(y0) e^{-y0^2}/n!, n <= 8), from long double on
+// the host.  Two Horner chains on loaded coefficients: no fp64 constants to
+// materialise (each costs two scalar moves per use), half the VALU work.
+struct CoefTab {
+    const double* __restrict__ p;
+};
+
+__device__ __forceinline__ ErfExp erf_gauss(double y, CoefTab tab) {
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const double ay = fmin(fabs(y), 8.0);
+    const double jd = rint(ay * 64.0);
+    const int j = (int)jd;
+    const double h = ay - jd * (1.0 / 64.0);
+    const d2v* c = (const d2v*)(tab.p + (size_t)j * kCoefStride);
+    const d2v v0 = c[0], v1 = c[1], v2 = c[2], v3 = c[3];
+    const d2v v4 = c[4], v5 = c[5], v6 = c[6], v7 = c[7], v8 = c[8];
+    double e = fma(v3[1], h, v3[0]);
+    e = fma(e, h, v2[1]);
+    e = fma(e, h, v2[0]);
+    e = fma(e, h, v1[1]);
+    e = fma(e, h, v1[0]);
+    e = fma(e, h, v0[1]);
+    e = fma(e, h, v0[0]);
+    double g = fma(v8[0], h, v7[1]);
+    g = fma(g, h, v7[0]);
+    g = fma(g, h, v6[1]);
+    g = fma(g, h, v6[0]);
+    g = fma(g, h, v5[1]);
+    g = fma(g, h, v5[0]);
+    g = fma(g, h, v4[1]);
+    g = fma(g, h, v4[0]);
+    const bool big = fabs(y) > 8.0;
+    ErfExp r;
+    r.erf = copysign(big ? 1.0 : e, y);
+    r.g = big ? 0.0 : g;
     return r;
 }
 

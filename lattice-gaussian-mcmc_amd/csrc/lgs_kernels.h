@@ -11,7 +11,8 @@ constexpr unsigned int kFlagOverflow = 2u;   // |z| >= 2^31 with an int32 store
 constexpr unsigned int kFlagI8Range = 4u;    // |z| > 32639: int8-digit B z must be redone in fp64
 constexpr unsigned int kFlagOverflow16 = 8u; // |z| > 32767 in a 16-bit internal store
 
-constexpr int kErfTabLast = 512;  // SampleZ erf/exp table: y_j = j/64, j = 0..kErfTabLast (y <= 8)
+constexpr int kErfTabLast = 512;
+constexpr int kCoefStride = 18;  // doubles per grid point of the coefficient table (lgs_device.h CoefTab)  // SampleZ erf/exp table: y_j = j/64, j = 0..kErfTabLast (y <= 8)
 
 // Per-coordinate SampleZ constants (kSzcStride doubles per coordinate, built by
 // the host in lgs_set_basis; lgs_device.h sample_z_coord):
@@ -82,6 +83,7 @@ struct KleinArgs {
     double* LW;
     unsigned int* flags;
     const double* etab;  // SampleZ erf/exp table (nullptr: ocml libm path)
+    const double* etab2; // its Taylor-coefficient form (lgs_device.h CoefTab)
     const double* szc;   // per-coordinate SampleZ constants (nullptr: generic sample_z)
     const double* crec;  // per-coordinate records (kRecStride doubles, layout above)
     // int8-digit far field (nullptr rd: fp64 MFMA far field)

@@ -112,10 +112,31 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         zi = (double)o.z;
         if (WL) lw += o.log_norm;
     } else {
-        double ln;
-        zi = sample_z_coord(mu, rs.u((uint32_t)(a.d - 1 - i)), rec, a.precision,
-                            a.linear_probs != 0, WL, etab, ln);
-        if (WL) lw += ln;
+        // inline two-point decision of the small kind (see sample_z_coord): when one
+        // weight is exactly 0 the decision does not depend on u, so no draw is made
+        // (draws are counter-addressed: skipping one shifts nothing)
+        bool done = false;
+#ifdef LGS_INLINE_SMALL  // measured slower (register pressure in the near field)
+        if ((int)rec[2] == kSzSmall) {
+            const double lo = floor(mu - rec[6]), hi = ceil(mu + rec[6]);
+            if (hi - lo == 1.0) {
+                const double t0 = (lo - mu) * rec[1], t1 = (hi - mu) * rec[1];
+                const double e0 = -0.5 * (t0 * t0), e1 = -0.5 * (t1 * t1);
+                const double em = fmax(e0, e1);
+                if (fmin(e0, e1) - em < -745.2 && !(a.linear_probs && em < -745.2)) {
+                    zi = e0 > e1 ? lo : hi;
+                    if (WL) lw += em;
+                    done = true;
+                }
+            }
+        }
+#endif
+        if (!done) {
+            double ln;
+            zi = sample_z_coord(mu, rs.u((uint32_t)(a.d - 1 - i)), rec, a.precision,
+                                a.linear_probs != 0, WL, etab, ln);
+            if (WL) lw += ln;
+        }
     }
     if (!WL) {
         const double res = zi - mu;
@@ -448,12 +469,21 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
     // as LDS) to leave LDS for the block-shared R-digit slab of the far field
     __shared__ double tab_lds[OZ ? 2 : 2 * (kErfTabLast + 1)];
     __shared__ __attribute__((aligned(16))) int8_t ash[OZ ? 2 * 2 * kOzDigits * 1024 : 16];  // 2 x 14 KB
+#ifdef LGS_COEF_ON  // Taylor-coefficient table: measured 2% slower (load latency)
+    using ETP = std::conditional_t<OZ, CoefTab, lds_cdptr>;
+    ETP etab_s;
+    if constexpr (OZ)
+        etab_s = CoefTab{a.etab2};
+    else
+        etab_s = stage_etab(tab_lds, a.etab);
+#else
     using ETP = std::conditional_t<OZ, const double*, lds_cdptr>;
     ETP etab_s;
     if constexpr (OZ)
         etab_s = a.etab;
     else
         etab_s = stage_etab(tab_lds, a.etab);
+#endif
     // 32-row panels: the panel's per-coordinate records, staged block-wide
     __shared__ double rec_lds[PB == 32 ? 32 * kRecStride : 2];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -597,25 +627,51 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
             // sub-panels, so only 16 running sums are live across the SampleZ
             // calls (occupancy); the block R[L rows, U cols] that couples them is
             // applied with 16 MFMAs after the upper sub-panel U is decided.
+            // Coefficients are kept in registers and stored once per sub-panel: a store
+            // still in flight at a SampleZ call would be waited for at the callee's
+            // entry (the calling convention starts with s_waitcnt 0).
             auto near16 = [&](int rows16, int top) {
-                for (int s = 0; s < rows16; ++s) {
-                    const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
-                    const lds_cdptr rec = (lds_cdptr)rec_lds + (i - (p_hi - 32)) * kRecStride;
-                    const double mu = (rec[kRecCp] - acc[15]) * rec[kRecIrii];
-                    const double zi = decide_coord_rec<WL>(a, i, mu, rec, rs, lw, flags, etab_s);
-                    store_z(Z, (size_t)i * ldz + p, zi, flags);
-                    if constexpr (OZ) {  // int16 history for the int8-digit far field
-                        const int ih = i + a.h16_shift;
-                        if (!(zi <= 32767.0 && zi >= -32767.0)) flags |= kFlagOverflow16;
-                        a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] =
-                            (int16_t)fmin(fmax(zi, -32767.0), 32767.0);
+                using ZH = std::conditional_t<sizeof(ZT) == 8, double, int>;
+                ZH zh[16];
+#pragma unroll
+                for (int s = 0; s < 16; ++s) {
+                    if (s < rows16) {
+                        const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
+                        const lds_cdptr rec = (lds_cdptr)rec_lds + (i - (p_hi - 32)) * kRecStride;
+                        const double mu = (rec[kRecCp] - acc[15]) * rec[kRecIrii];
+                        const double zi = decide_coord_rec<WL>(a, i, mu, rec, rs, lw, flags, etab_s);
+                        if constexpr (sizeof(ZT) == 8) {
+                            zh[s] = zi;
+                        } else {
+                            if (sizeof(ZT) == 4 && !(zi <= 2147483647.0 && zi >= -2147483648.0))
+                                flags |= kFlagOverflow;
+                            if (sizeof(ZT) == 2 && !(zi <= 32767.0 && zi >= -32768.0)) flags |= kFlagOverflow16;
+                            zh[s] = (int)fmin(fmax(zi, -2147483648.0), 2147483647.0);
+                        }
+                        if constexpr (OZ)
+                            if (!(zi <= 32767.0 && zi >= -32767.0)) flags |= kFlagOverflow16;
+                        const lds_cdptr rc = rec + kRecRs;
+#pragma unroll
+                        for (int k = 0; k < 15; ++k) acc[k] = fma(rc[14 - k], zi, acc[k]);
+#pragma unroll
+                        for (int k = 15; k >= 1; --k) acc[k] = acc[k - 1];
+                        acc[0] = 0.0;
                     }
-                    const lds_cdptr rc = rec + kRecRs;
+                }
 #pragma unroll
-                    for (int k = 0; k < 15; ++k) acc[k] = fma(rc[14 - k], zi, acc[k]);
-#pragma unroll
-                    for (int k = 15; k >= 1; --k) acc[k] = acc[k - 1];
-                    acc[0] = 0.0;
+                for (int s = 0; s < 16; ++s) {
+                    if (s < rows16) {
+                        const int i = top - 1 - s;
+                        if constexpr (sizeof(ZT) == 8)
+                            Z[(size_t)i * ldz + p] = (ZT)(int64_t)zh[s];
+                        else
+                            Z[(size_t)i * ldz + p] = (ZT)zh[s];
+                        if constexpr (OZ) {  // int16 history for the int8-digit far field
+                            const int ih = i + a.h16_shift;
+                            const double zc = fmin(fmax((double)zh[s], -32767.0), 32767.0);
+                            a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] = (int16_t)zc;
+                        }
+                    }
                 }
             };
             near16(p_hi < 16 ? p_hi : 16, p_hi);

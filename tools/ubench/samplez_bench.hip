@@ -13,6 +13,10 @@ using namespace lgs;
 
 __constant__ double* szc;
 
+__device__ __noinline__ double trivial_call(double mu, double u, const double* q) {
+    return rint(mu + u * 1e-300) + q[0] * 0.0;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void sz_kernel(const double* __restrict__ sigs, int nc,
                                                  const double* __restrict__ etab, double* out) {
@@ -32,14 +36,15 @@ __global__ __launch_bounds__(256) void sz_kernel(const double* __restrict__ sigs
         const double s = sigs[i];
         int64_t z;
         if (MODE == 0) z = (int64_t)rint(mu + u * 1e-300);
+        else if (MODE == 5) z = (int64_t)trivial_call(mu, u, sigs + i);
         else if (MODE == 1) z = sample_z(mu, s, 10, false, u, false, etab).z;
         else if (MODE == 2) z = sample_z(mu, s, 10, false, u, false, nullptr).z;
         else if (MODE == 3) {
             double ln;
-            z = (int64_t)sample_z_coord(mu, u, szc + (size_t)i * kSzcStride, 10, false, false, etab, ln);
+            z = (int64_t)sample_z_coord(mu, u, cst(szc) + (size_t)i * kSzcStride, 10, false, false, etab, ln);
         } else {
             double ln;
-            z = (int64_t)sample_z_coord(mu, u, szc + (size_t)i * kSzcStride, 10, false, false,
+            z = (int64_t)sample_z_coord(mu, u, cst(szc) + (size_t)i * kSzcStride, 10, false, false,
                                         (lds_cdptr)tab_lds, ln);
         }
         acc += (double)z;
@@ -100,6 +105,7 @@ int main() {
         printf("--- waves/SIMD <= %d (dynamic LDS %d B)\n", occ, occ_lds);
         hipMemcpyToSymbol(HIP_SYMBOL(szc), &qw, sizeof(qw));
         run("philox+round (wide)", sz_kernel<0>, sig_w);
+        run("philox+trivial call", sz_kernel<5>, sig_w);
         run("wide  tab", sz_kernel<1>, sig_w);
         run("wide  libm", sz_kernel<2>, sig_w);
         run("wide  coord", sz_kernel<3>, sig_w);
