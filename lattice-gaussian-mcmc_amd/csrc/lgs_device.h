@@ -217,6 +217,9 @@ __device__ __noinline__ double em_P(double x, double mu, double sig, double is, 
 // the fp64 resolution of S >= 10 (sigma >= 4).  The table (8.2 KB) is read from
 // LDS in the Klein kernels (TP = lds pointer) and from global memory elsewhere.
 using lds_cdptr = const __attribute__((address_space(3))) double*;
+// Global-address-space pointer: global_load (vmcnt only) instead of flat_load,
+// which also counts against lgkmcnt.
+using gdptr = const __attribute__((address_space(1))) double*;
 
 struct ErfExp {
     double erf, g;  // erf(y), exp(-y^2)
@@ -549,11 +552,9 @@ __device__ __forceinline__ double sample_z_wide(double mu, double u, QP q,
         fk = gauss_tab(kd, m, is, etab);
     }
     const double margin = fmin(Ck - target, kd > a ? target - (Ck - fk) : target);
-    if (!(margin > 1e-12 * S) || !(Ck > target)) {
-        const SampleZOut o = sample_z_table(mu, sig, precision, linear_probs, u, want_log);
-        log_norm = o.log_norm;
-        return (double)o.z;
-    }
+    // too close to call in fp64 (margin below 1e-12 S): sample_z_coord finishes
+    // it with the exact table walk
+    if (!(margin > 1e-12 * S) || !(Ck > target)) return __builtin_nan("");
     log_norm = want_log ? log(S) : 0.0;
     return c + kd;
 }
@@ -591,21 +592,23 @@ __device__ __forceinline__ cdptr uniformize(cdptr p) {
 }
 __device__ __forceinline__ lds_cdptr uniformize(lds_cdptr p) { return p; }
 
+// The per-coordinate decision proper is a leaf function: it makes no calls, so
+// it needs no frame (a non-leaf callee saves its return address through a
+// scratch store and reload on every call).  The rare cases it does not
+// handle -- small-kind windows of more than 4 points, the generic kind and wide
+// decisions within 1e-12 S of a boundary -- return NaN, and sample_z_coord
+// below finishes them out of line.
 template <typename TP, typename QP>
-LGS_SAMPLEZ_ATTR double sample_z_coord(double mu, double u, QP qin, int precision,
-                                       bool linear_probs, bool want_log, TP etab,
-                                       double& log_norm) {
+__device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qin, int precision,
+                                                      bool linear_probs, bool want_log, TP etab,
+                                                      double& log_norm) {
     const QP q = uniformize(qin);  // all lanes are on the same coordinate
     const int kind = (int)q[2];
     const double sig = q[0];
     if (kind == kSzSmall) {
         const double lo = floor(mu - q[6]);
         const double hi = ceil(mu + q[6]);
-        if (hi - lo > 3.0) {
-            const SampleZOut o = sample_z_table(mu, sig, precision, linear_probs, u, want_log);
-            log_norm = o.log_norm;
-            return (double)o.z;
-        }
+        if (hi - lo > 3.0) return __builtin_nan("");
         const double is = q[1];
         if (hi - lo == 1.0) {
             // two points whose weights differ by more than e^745.2: the smaller
@@ -653,14 +656,49 @@ LGS_SAMPLEZ_ATTR double sample_z_coord(double mu, double u, QP qin, int precisio
         log_norm = want_log ? emax + log(Ssum) : 0.0;
         return z;
     }
-    if (kind == kSzGeneric) {
-        const SampleZOut o = sample_z_generic(mu, sig, precision, linear_probs, u, want_log, etab);
-        log_norm = o.log_norm;
-        return (double)o.z;
-    }
+    if (kind == kSzGeneric) return __builtin_nan("");
     return sig < 50.0
                ? sample_z_wide<6>(mu, u, q, kind, precision, linear_probs, want_log, etab, log_norm)
                : sample_z_wide<3>(mu, u, q, kind, precision, linear_probs, want_log, etab, log_norm);
+}
+
+// Both results come back in registers (a reference parameter of a call lives in
+// the caller's scratch frame: a store per call that the next call waits for).
+struct SzPair {
+    double z, ln;
+};
+template <typename TP, typename QP>
+LGS_SAMPLEZ_ATTR SzPair sample_z_coord_leaf(double mu, double u, QP q, int precision,
+                                            bool linear_probs, bool want_log, TP etab) {
+    SzPair r;
+    r.ln = 0.0;
+    r.z = sample_z_coord_body(mu, u, q, precision, linear_probs, want_log, etab, r.ln);
+    return r;
+}
+
+template <typename TP>
+__device__ __noinline__ double sample_z_coord_fallback(double mu, double u, double sig, int kind,
+                                                       int precision, bool linear_probs,
+                                                       bool want_log, TP etab, double& log_norm) {
+    const SampleZOut o = kind == kSzGeneric
+                             ? sample_z_generic(mu, sig, precision, linear_probs, u, want_log, etab)
+                             : sample_z_table(mu, sig, precision, linear_probs, u, want_log);
+    log_norm = o.log_norm;
+    return (double)o.z;
+}
+
+// SampleZ for one coordinate from its precomputed constants (kinds in lgs_kernels.h).
+template <typename TP, typename QP>
+__device__ __forceinline__ double sample_z_coord(double mu, double u, QP q, int precision,
+                                                 bool linear_probs, bool want_log, TP etab,
+                                                 double& log_norm) {
+    const SzPair r = sample_z_coord_leaf(mu, u, q, precision, linear_probs, want_log, etab);
+    double z = r.z;
+    log_norm = r.ln;
+    if (__builtin_isnan(z))
+        z = sample_z_coord_fallback(mu, u, q[0], (int)q[2], precision, linear_probs, want_log, etab,
+                                    log_norm);
+    return z;
 }
 
 }  // namespace lgs

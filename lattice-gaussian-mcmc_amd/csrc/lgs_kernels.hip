@@ -88,7 +88,7 @@ template <bool WL, typename TP>
 __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, double mu,
                                                    lds_cdptr rec, CoordStream& rs, double& lw,
                                                    unsigned int& flags, TP etab) {
-    double zi;
+    double zi = 0.0;
     if (!isfinite(mu)) {
         flags |= kFlagNonFinite;
         return 0.0;
@@ -477,10 +477,10 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
     else
         etab_s = stage_etab(tab_lds, a.etab);
 #else
-    using ETP = std::conditional_t<OZ, const double*, lds_cdptr>;
+    using ETP = std::conditional_t<OZ, gdptr, lds_cdptr>;
     ETP etab_s;
     if constexpr (OZ)
-        etab_s = a.etab;
+        etab_s = (gdptr)a.etab;
     else
         etab_s = stage_etab(tab_lds, a.etab);
 #endif
