@@ -527,10 +527,9 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     }
     // int8-digit far field (klein_mfma_kernel OZ): per 32-row panel, rows scaled by
     // 2^E_i (|R_ij| 2^-E_i < 1/4 over the panel's far columns j >= p_hi) and split
-    // into 7 balanced base-256 digits (54 significant bits); the row's correction
-    // 128 * sum_j R~_ij (R~ = the digit approximation) is kept in long double.
+    // into 7 balanced base-256 digits (54 significant bits).
     const int64_t npan32 = (d + 31) / 32;
-    std::vector<double> rscale(dd, 1.0), rcorr(dd, 0.0);
+    std::vector<double> rscale(dd, 1.0);
     std::vector<int64_t> rdoff(npan32 + 1, 0);
     std::vector<int8_t> rdv;
     bool oz = d <= lgs::kOzMaxD;
@@ -550,11 +549,9 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
                 for (int64_t j = p_hi; j < d; ++j) mx = std::max(mx, std::fabs(R[(size_t)row * dd + j]));
                 const int E = mx > 0.0 ? std::ilogb(mx) + 3 : 0;
                 rscale[row] = std::ldexp(1.0, E);
-                long double corr = 0.0L;
                 const int t = r >> 4, n = r & 15;
                 for (int64_t j = p_hi; j < d; ++j) {
                     long long M = std::llrint(std::ldexp(R[(size_t)row * dd + j], 56 - E));
-                    corr += (long double)M;
                     const int64_t kk = j - p_hi, ch = kk / 64, h = (kk % 64) / 16, e = kk % 16;
                     for (int a = lgs::kOzDigits; a >= 1; --a) {  // least significant digit first
                         const long long dg = ((M % 256) + 256 + 128) % 256 - 128;
@@ -564,7 +561,6 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
                     }
                     if (M != 0) return fail(LGS_ERR_INVALID, "R digit split overflow");
                 }
-                rcorr[row] = (double)(128.0L * std::ldexp(corr, E - 56));
             }
             (void)nch;
         }
@@ -581,7 +577,6 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
         r[lgs::kRecLterm] = co[4 * dd + i];
         std::copy(rsv.data() + i * 15, rsv.data() + i * 15 + 15, r + lgs::kRecRs);
         r[lgs::kRecScale] = rscale[i];
-        r[lgs::kRecCorr] = rcorr[i];
     }
     c->has_rd = oz;
     if (oz) {

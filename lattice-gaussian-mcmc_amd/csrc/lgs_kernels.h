@@ -32,9 +32,9 @@ constexpr int kSzcStride = 24;
 // Staged into LDS once per 32-row panel by klein_mfma_kernel.
 constexpr int kRecCp = kSzUsed, kRecIrii = kSzUsed + 1, kRecRos = kSzUsed + 2,
               kRecIsr = kSzUsed + 3, kRecLterm = kSzUsed + 4, kRecRs = kSzUsed + 5;
-// int8-digit far field (klein_mfma_kernel OZ): row scale 2^E_i and the offset
-// correction 128 * sum_j R~_ij of the coordinate's row over its panel's far columns
-constexpr int kRecScale = kRecRs + 15, kRecCorr = kRecRs + 16;
+// int8-digit far field (klein_mfma_kernel OZ): row scale 2^E_i of the
+// coordinate's row over its panel's far columns
+constexpr int kRecScale = kRecRs + 15;
 constexpr int kRecStride = kRecRs + 18;  // 44: 352 bytes, 16-byte multiple
 // int8-digit far field layout: per 32-row panel pk >= 1 (K = 32 pk far columns,
 // ceil(K/64) chunks of 64): [chunk][row tile t][digit a][lane][16 bytes]

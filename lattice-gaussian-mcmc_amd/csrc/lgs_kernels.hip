@@ -313,12 +313,15 @@ struct ZQuad<int64_t> {
 // F_i = sum_{j >= p_hi} R_ij x_j for the 32 rows of panel pk and the wave's 64
 // samples, exactly enough to stand in for fp64: rows scaled by 2^E_i and split
 // into 7 balanced base-256 digits r_a (|R 2^-E| < 1/4, 54 significant bits,
-// host: lgs_set_basis); coefficients x in [-32767, 32767] from the int16 history,
-// x = 256 x1 + x0 + 128 with x1 = the high byte and x0 = low byte ^ 0x80 (both
-// signed), so a digit plane is two byte permutes of the raw int16 pairs.  Class
-// c = a - b of r_a x_b (weight 256^-c) is summed exactly in int32 on
-// v_mfma_i32_16x16x64_i8 (|sum| <= 2 K 2^14 < 2^31 for d <= 32768); then
-// F_i = 2^E_i sum_c 256^-c C_c + 128 sum_j R~_ij (host-precomputed).
+// host: lgs_set_basis); coefficients x in [-32767, 32639] held in the int16
+// history as y = x + 128, so x = 256 x1 + x0 with x1 = the high byte of y and
+// x0 = low byte ^ 0x80 (both signed): a digit plane is two byte permutes of the
+// raw int16 pairs, and x = 0 gives two zero planes.  Class c = a - b of r_a x_b
+// (weight 256^-c) is summed exactly in int32 on v_mfma_i32_16x16x64_i8
+// (|sum| <= 2 K 2^14 < 2^31 for d <= 32768); then F_i = 2^E_i sum_c 256^-c C_c.
+// Chunks whose two 32-row panels are zero in every sample of the block (bits of
+// nzm, set by the near field) contribute nothing and are skipped: no history
+// read, no slab, no MFMA.
 // Four passes (16 samples each) keep 2 row tiles x 8 classes = 64 accumulator
 // VGPRs.  Row tile 1 (the upper sub-panel) goes to acc through the LDS tile;
 // tile 0 is parked in the per-wave scratch f0 and moved into the LDS tile once
@@ -327,9 +330,20 @@ typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_hi, int64_t p0, int lane,
                                              lds_cdptr rec, double* F, int LDF, double (&acc)[16],
-                                             int8_t* ash) {
+                                             int8_t* ash, const uint32_t* nzm) {
     const int d = a.d;
     const int K = d - p_hi, nch = (K + 63) / 64;
+    // chunk ch covers panels pk-1-2ch and pk-2-2ch (panel q: rows d-32(q+1) .. d-32q-1)
+    auto live = [&](int ch) -> bool {
+        const int q0 = pk - 1 - 2 * ch, q1 = q0 - 1;
+        uint32_t b = nzm[q0 >> 5] >> (q0 & 31);
+        if (q1 >= 0) b |= nzm[q1 >> 5] >> (q1 & 31);
+        return (__builtin_amdgcn_readfirstlane(b) & 1u) != 0;
+    };
+    auto next_live = [&](int ch) {
+        while (ch < nch && !live(ch)) ++ch;
+        return ch;
+    };
     const int h = lane >> 4, n = lane & 15, tid = threadIdx.x;
     // block-shared R-digit slab of one 64-column chunk (both row tiles): 896 x 16 B,
     // double-buffered in LDS; thread tid stages pieces tid + 256 m (m < 4, < 896)
@@ -365,21 +379,30 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int c = 0; c < 8; ++c) cc[q][t][c] = (v4i32_t){0, 0, 0, 0};
-        const int16_t* __restrict__ hp0 = a.h16 + (blk0 * a.h16_lanes + p0 + 32 * gp + n) * 16;
-        const int16_t* __restrict__ hp1 = hp0 + 16 * 16;  // group 2gp + 1: 16 lanes further
+        const int16_t* __restrict__ hb0 = a.h16 + (blk0 * a.h16_lanes + p0 + 32 * gp + n) * 16;
+        const int16_t* __restrict__ hb1 = hb0 + 16 * 16;  // group 2gp + 1: 16 lanes further
         v4i32_t pf[4];
-        __syncthreads();  // previous pass done with both buffers
-        slab_load(0, pf);
-        slab_store(0, pf);
-        if (nch > 1) slab_load(1, pf);
         v4u_t w[2][2];
-        w[0][0] = __builtin_nontemporal_load((const v4u_t*)hp0);
-        w[0][1] = __builtin_nontemporal_load((const v4u_t*)hp0 + 1);
-        w[1][0] = __builtin_nontemporal_load((const v4u_t*)hp1);
-        w[1][1] = __builtin_nontemporal_load((const v4u_t*)hp1 + 1);
+        auto hist_load = [&](int ch) {
+            const v4u_t* h0 = (const v4u_t*)(hb0 + (size_t)ch * hstep);
+            const v4u_t* h1 = (const v4u_t*)(hb1 + (size_t)ch * hstep);
+            w[0][0] = __builtin_nontemporal_load(h0);
+            w[0][1] = __builtin_nontemporal_load(h0 + 1);
+            w[1][0] = __builtin_nontemporal_load(h1);
+            w[1][1] = __builtin_nontemporal_load(h1 + 1);
+        };
+        __syncthreads();  // previous pass done with both buffers
+        int cur = next_live(0);
+        int nxt = cur < nch ? next_live(cur + 1) : nch;
+        if (cur < nch) {
+            slab_load(cur, pf);
+            slab_store(0, pf);
+            if (nxt < nch) slab_load(nxt, pf);
+            hist_load(cur);
+        }
         __syncthreads();
 #pragma unroll 1
-        for (int ch = 0; ch < nch; ++ch) {
+        for (int it = 0; cur < nch; ++it) {
             v4i32_t xh[2], xl[2];  // history of chunk ch -> digit planes, per group
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
@@ -393,17 +416,13 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
                 xl[q][2] = (int)(__builtin_amdgcn_perm(w1[1], w1[0], 0x06040200u) ^ 0x80808080u);
                 xl[q][3] = (int)(__builtin_amdgcn_perm(w1[3], w1[2], 0x06040200u) ^ 0x80808080u);
             }
-            if (ch + 1 < nch) {  // history of the next chunk; slab ch+1 -> LDS, fetch slab ch+2
-                hp0 += hstep;
-                hp1 += hstep;
-                w[0][0] = __builtin_nontemporal_load((const v4u_t*)hp0);
-                w[0][1] = __builtin_nontemporal_load((const v4u_t*)hp0 + 1);
-                w[1][0] = __builtin_nontemporal_load((const v4u_t*)hp1);
-                w[1][1] = __builtin_nontemporal_load((const v4u_t*)hp1 + 1);
-                slab_store((ch + 1) & 1, pf);
-                if (ch + 2 < nch) slab_load(ch + 2, pf);
+            const int nxt2 = nxt < nch ? next_live(nxt + 1) : nch;
+            if (nxt < nch) {  // history of the next live chunk; its slab -> LDS, fetch the one after
+                hist_load(nxt);
+                slab_store((it + 1) & 1, pf);
+                if (nxt2 < nch) slab_load(nxt2, pf);
             }
-            const v4i32_t* sl = ash4 + (ch & 1) * SLAB + lane;
+            const v4i32_t* sl = ash4 + (it & 1) * SLAB + lane;
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -417,7 +436,9 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
                             __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xl[q], cc[q][t][dg + 1], 0, 0, 0);
                     }
                 }
-            __syncthreads();  // slab ch+1 complete; slab ch reads done before it is reused
+            __syncthreads();  // next slab complete; this one's reads done before it is reused
+            cur = nxt;
+            nxt = nxt2;
         }
         // classes -> fp64; D layout: rows 4h + reg of the tile, sample 16g + n
 #pragma unroll
@@ -431,8 +452,7 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
                     double sv = (double)cc[q][t][7][reg];
 #pragma unroll
                     for (int c = 6; c >= 0; --c) sv = fma(sv, 0.00390625, (double)cc[q][t][c][reg]);
-                    const lds_cdptr rr = rec + row * kRecStride;
-                    const double fv = fma(sv, rr[kRecScale], rr[kRecCorr]);
+                    const double fv = sv * rec[row * kRecStride + kRecScale];
                     if (t == 1) {
                         F[(4 * h + reg) * LDF + 16 * g + n] = fv;
                     } else {
@@ -486,6 +506,10 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
 #endif
     // 32-row panels: the panel's per-coordinate records, staged block-wide
     __shared__ double rec_lds[PB == 32 ? 32 * kRecStride : 2];
+    // OZ: bit q set when panel q has a nonzero coefficient in some sample of the block
+    __shared__ uint32_t nzm[OZ ? kOzMaxD / 32 / 32 : 1];
+    if constexpr (OZ)
+        for (int e = threadIdx.x; e < kOzMaxD / 32 / 32; e += 256) nzm[e] = 0u;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t p0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
     const bool active = p0 < a.n;  // whole waves only (n % 64 == 0)
@@ -528,7 +552,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
           if constexpr (OZ && PB == 32) {
-            oz_far_field(a, pk, p_hi, p0, lane, (lds_cdptr)rec_lds, F, LDF, acc, ash);
+            oz_far_field(a, pk, p_hi, p0, lane, (lds_cdptr)rec_lds, F, LDF, acc, ash, nzm);
             (void)NT;
           } else {
             d4_t f[NT][4];
@@ -630,6 +654,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
             // Coefficients are kept in registers and stored once per sub-panel: a store
             // still in flight at a SampleZ call would be waited for at the callee's
             // entry (the calling convention starts with s_waitcnt 0).
+            bool pnz = false;  // (OZ) a nonzero coefficient in this panel, this lane
             auto near16 = [&](int rows16, int top) {
                 using ZH = std::conditional_t<sizeof(ZT) == 8, double, int>;
                 ZH zh[16];
@@ -649,7 +674,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
                             zh[s] = (int)fmin(fmax(zi, -2147483648.0), 2147483647.0);
                         }
                         if constexpr (OZ)
-                            if (!(zi <= 32767.0 && zi >= -32767.0)) flags |= kFlagOverflow16;
+                            if (!(zi <= 32639.0 && zi >= -32767.0)) flags |= kFlagOverflow16;
                         const lds_cdptr rc = rec + kRecRs;
 #pragma unroll
                         for (int k = 0; k < 15; ++k) acc[k] = fma(rc[14 - k], zi, acc[k]);
@@ -666,10 +691,12 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
                             Z[(size_t)i * ldz + p] = (ZT)(int64_t)zh[s];
                         else
                             Z[(size_t)i * ldz + p] = (ZT)zh[s];
-                        if constexpr (OZ) {  // int16 history for the int8-digit far field
+                        if constexpr (OZ) {  // int16 history (z + 128) for the int8-digit far field
                             const int ih = i + a.h16_shift;
-                            const double zc = fmin(fmax((double)zh[s], -32767.0), 32767.0);
-                            a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] = (int16_t)zc;
+                            const double zc = fmin(fmax((double)zh[s], -32767.0), 32639.0);
+                            a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] =
+                                (int16_t)(int)(zc + 128.0);
+                            pnz |= zh[s] != 0;
                         }
                     }
                 }
@@ -704,6 +731,9 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 near16(rows_l, p_hi - 16);
+            }
+            if constexpr (OZ) {  // visible to the block at the next panel's staging barrier
+                if (__builtin_amdgcn_ballot_w64(pnz) != 0 && lane == 0) atomicOr(&nzm[pk >> 5], 1u << (pk & 31));
             }
         } else {
             for (int s = 0; s < rows; ++s) {

@@ -136,9 +136,42 @@ def test_int8_digit_far_field_matches_fp64_far_field(ctx, ctx_far64, oracle):
     assert np.array_equal(out[0][:64], o["z"])
 
 
+def test_int8_digit_far_field_zero_panel_skip(ctx, oracle):
+    """Far-field chunks whose panels are zero in every sample of a block are
+    skipped.  Panels 1, 2 and 5 (rows d-32(q+1) .. d-32q-1) are pinned to z = 0
+    (sigma_i ~ 3e-4); one row of panel 6 is a centred sigma_i = 0.25 coordinate, so
+    it is nonzero in only a few samples of a few 256-sample blocks: those blocks
+    must keep the chunk, the others skip it.  Bit-exact against the oracle."""
+    rng = np.random.default_rng(17)
+    d, sigma, n = 320, 3.0, 4096
+    R = np.triu(rng.normal(size=(d, d)) * 0.3, 1)
+    R[np.diag_indices(d)] = rng.uniform(0.5, 2.0, d)
+    cp = rng.normal(size=d)
+    for q in (1, 2, 5):
+        rows = np.arange(d - 32 * (q + 1), d - 32 * q)
+        R[rows, rows] = 1e4
+        cp[rows] = 0.0
+    rare = d - 32 * 7 + 5  # in panel 6
+    q6 = np.arange(d - 32 * 7, d - 32 * 6)
+    R[q6, q6] = 1e4
+    cp[q6] = 0.0
+    R[rare, rare + 1:] = 0.0
+    R[rare, rare] = sigma / 0.25
+    ctx.set_basis(R, cp, None, sigma)
+    r = ctx.klein_host(23, 0, n, want_z=True, want_v=False)["z"]
+    o = oracle.klein(R, cp, sigma, n, seed=23, first_sample=0)["z"]
+    for q in (1, 2, 5):
+        assert not o[:, d - 32 * (q + 1):d - 32 * q].any()
+    hits = np.flatnonzero(o[:, rare])
+    blocks = np.unique(hits // 256)
+    assert 0 < len(blocks) < n // 256, (hits, blocks)
+    assert not np.delete(o[:, q6], rare - q6[0], axis=1).any()
+    assert np.array_equal(r, o)
+
+
 def test_int8_digit_far_field_overflow_falls_back(capi, oracle):
-    """|z| > 32767 cannot use the int16 history: the launch is redone with the fp64
-    far field (same counters) and the context keeps it."""
+    """|z| > 32639 cannot use the int16 history (it holds z + 128): the launch is
+    redone with the fp64 far field (same counters) and the context keeps it."""
     rng = np.random.default_rng(5)
     d = 96
     R = np.triu(rng.normal(size=(d, d)) * 0.01, 1)
