@@ -476,6 +476,19 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
 #ifndef LGS_MFMA_LB32
 #define LGS_MFMA_LB32 3
 #endif
+// Diagnostic builds (-DLGS_DIAG_CYCLES): per-wave shader-clock accounting of the
+// 32-row-panel kernel, summed over waves into lgs_diag_cycles (lane 0 adds):
+// [0] record staging + barriers, [1] far field, [2] near field, [3 + kind] the
+// SampleZ decision (with its Philox draw) per SampleZ kind, [8 + kind] decisions
+// per kind, [13] whole kernel.
+#ifdef LGS_DIAG_CYCLES
+__device__ unsigned long long lgs_diag_cycles[16];
+#define LGS_DC_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define LGS_DC_ADD(k, x) dc[k] += (x)
+#else
+#define LGS_DC_T(v)
+#define LGS_DC_ADD(k, x)
+#endif
 // OZ (32-row panels only): far field as an exact int8-digit product on
 // v_mfma_i32_16x16x64_i8 instead of fp64 MFMA (see oz_far_field).
 template <typename ZT, int PB, bool WL, bool OZ = false>
@@ -511,6 +524,10 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
     if constexpr (OZ)
         for (int e = threadIdx.x; e < kOzMaxD / 32 / 32; e += 256) nzm[e] = 0u;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#ifdef LGS_DIAG_CYCLES
+    uint64_t dc[16] = {};
+#endif
+    LGS_DC_T(t_kernel0);
     const int64_t p0 = ((int64_t)blockIdx.x * 4 + wave) * 64;
     const bool active = p0 < a.n;  // whole waves only (n % 64 == 0)
     if (!active && PB != 32) return;  // (32-row panels: idle waves still stage records)
@@ -531,6 +548,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
     for (int pk = 0; pk < npan; ++pk) {
         const int p_hi = d - pk * PB;
         const int rows = p_hi < PB ? p_hi : PB;
+        LGS_DC_T(t_panel0);
         if constexpr (PB == 32) {
             // records of coordinates r0 .. r0+31 (r0 = p_hi - 32; negative ones skipped)
             __syncthreads();
@@ -542,6 +560,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
             __syncthreads();
             if (!active) continue;
         }
+        LGS_DC_T(t_far0);
+        LGS_DC_ADD(0, t_far0 - t_panel0);
 #ifdef LGS_DIAG_NO_FAR
         if (false) {
 #else
@@ -646,6 +666,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
                 for (int r = 0; r < 16; ++r) F[r * LDF + lane] = 0.0;
             }
         }
+        LGS_DC_T(t_near0);
+        LGS_DC_ADD(1, t_near0 - t_far0);
         if constexpr (PB == 32) {
             // Two-level near field: the 32-row panel is decided as two 16-row
             // sub-panels, so only 16 running sums are live across the SampleZ
@@ -664,7 +686,16 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
                         const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
                         const lds_cdptr rec = (lds_cdptr)rec_lds + (i - (p_hi - 32)) * kRecStride;
                         const double mu = (rec[kRecCp] - acc[15]) * rec[kRecIrii];
+                        LGS_DC_T(t_sz0);
                         const double zi = decide_coord_rec<WL>(a, i, mu, rec, rs, lw, flags, etab_s);
+#ifdef LGS_DIAG_CYCLES
+                        {
+                            LGS_DC_T(t_sz1);
+                            const int kind = (int)rec[2] & 7;
+                            LGS_DC_ADD(3 + kind, t_sz1 - t_sz0);
+                            LGS_DC_ADD(8 + kind, 1);
+                        }
+#endif
                         if constexpr (sizeof(ZT) == 8) {
                             zh[s] = zi;
                         } else {
@@ -735,6 +766,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
             if constexpr (OZ) {  // visible to the block at the next panel's staging barrier
                 if (__builtin_amdgcn_ballot_w64(pnz) != 0 && lane == 0) atomicOr(&nzm[pk >> 5], 1u << (pk & 31));
             }
+            LGS_DC_T(t_near1);
+            LGS_DC_ADD(2, t_near1 - t_near0);
         } else {
             for (int s = 0; s < rows; ++s) {
                 const int i = p_hi - 1 - s;
@@ -754,6 +787,12 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void 
     if (!active) return;
     if (a.LW) a.LW[p] = lw;
     if (flags) atomicOr(a.flags, flags);
+#ifdef LGS_DIAG_CYCLES
+    LGS_DC_T(t_kernel1);
+    dc[13] = t_kernel1 - t_kernel0;
+    if (lane == 0)
+        for (int k = 0; k < 16; ++k) atomicAdd(&lgs_diag_cycles[k], (unsigned long long)dc[k]);
+#endif
 }
 
 // ------------------------------------------------------------ log density
@@ -1110,13 +1149,21 @@ __global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z,
                                                     const int8_t* __restrict__ Bd0, int dc, int d,
                                                     int64_t n, double* __restrict__ V, int64_t ldv,
                                                     int64_t rb, int64_t rstride, int64_t roff,
-                                                    unsigned int* flags) {
+                                                    unsigned int* flags, int tx_count, int64_t ty_count) {
     constexpr int BM = 64, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
     __shared__ __attribute__((aligned(16))) int8_t Zs1[BM * P], Zs0[BM * P], Bs1[BN * P], Bs0[BN * P];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
-    const int r0 = blockIdx.x * BN;
-    const int64_t s0 = (int64_t)blockIdx.y * BM;
+    // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs, so
+    // workgroup b runs on XCD b % 8; the tx_count coordinate tiles of one sample
+    // tile are given to consecutive workgroups of the same XCD, which then reads
+    // that sample tile's coefficients from HBM once and from its own L2 after.
+    const int64_t b = blockIdx.x, w = b >> 3;
+    const int64_t ty = (w / tx_count) * 8 + (b & 7);
+    const int tx = (int)(w % tx_count);
+    if (ty >= ty_count) return;
+    const int r0 = tx * BN;
+    const int64_t s0 = ty * BM;
     v16i_t p1[2], p2[2], p3[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -1129,7 +1176,7 @@ __global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z,
     const int64_t zs_ = s0 + zm;
     const int64_t zcol = zs_ < n ? (sel ? sel[zs_] : zs_) : 0;  // this thread's sample column
     // only the K chunks where this row tile of B has a non-zero digit (exact skip)
-    const int ci0 = koff[blockIdx.x], ci1 = koff[blockIdx.x + 1];
+    const int ci0 = koff[tx], ci1 = koff[tx + 1];
     for (int ci = ci0; ci < ci1; ++ci) {
         const int c0 = kchunk[ci] * KC;
         {  // z chunk -> balanced base-256 digits, [sample][k] byte planes
@@ -1202,7 +1249,7 @@ __global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z,
             const int r = r0 + wn * 64 + tn * 32 + (lane & 31);
             if (r < d) {
                 const long long v = 65536LL * p1[tn][reg] + 256LL * p2[tn][reg] + (long long)p3[tn][reg];
-                vrow[r] = (double)v;
+                __builtin_nontemporal_store((double)v, vrow + r);  // streamed out, not re-read
             }
         }
     }
@@ -1362,10 +1409,24 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((d + 127) / 128), (unsigned)((n + 63) / 64));
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags));
+    const int tx = (d + 127) / 128;
+    const int64_t ty = (n + 63) / 64;
+    const dim3 grid((unsigned)(tx * ((ty + 7) / 8) * 8));  // whole rounds of 8 XCDs (extra tiles exit)
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty));
     return hipGetLastError();
 }
 
 }  // namespace launch
 }  // namespace lgs
+
+#ifdef LGS_DIAG_CYCLES
+// Diagnostic builds only (not part of include/lgs.h): read and reset the cycle sums.
+extern "C" __attribute__((visibility("default"))) int lgs_diag_cycles_read(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lgs::lgs_diag_cycles), 16 * sizeof(unsigned long long)) !=
+        hipSuccess)
+        return -1;
+    unsigned long long zero[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lgs::lgs_diag_cycles), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif

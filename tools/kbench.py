@@ -30,13 +30,28 @@ def run_one(args):
     lw = torch.empty(n, dtype=torch.float64, device="cuda:0")
     flags = _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR | (_capi.LGS_EXACT_ORDER if args.exact else 0)
     ctx.klein(1, 0, n, z, None, lw, flags)
+    import ctypes
+    diag = getattr(_capi.load_library(), "lgs_diag_cycles_read", None)
+    dbuf = (ctypes.c_ulonglong * 16)()
+    if diag is not None:
+        diag(dbuf)  # reset after the warm-up launch
     ctx.timing_enable(True)
     for r in range(args.reps):
         ctx.klein(1, (r + 1) * n, n, z, None, lw, flags)
     ms, k = ctx.timing_get(_capi.KERNEL_KLEIN)
     avg = ms / k
-    print(json.dumps({"lib": os.environ.get("LGS_LIB", "default"), "config": args.config, "d": d, "n": n,
-                      "kernel_ms": round(avg, 3), "samples_per_s": round(n / avg * 1e3, 1)}), flush=True)
+    out = {"lib": os.environ.get("LGS_LIB", "default"), "config": args.config, "d": d, "n": n,
+           "kernel_ms": round(avg, 3), "samples_per_s": round(n / avg * 1e3, 1)}
+    if diag is not None:
+        diag(dbuf)
+        waves = args.reps * n // 64
+        names = ["stage", "far", "near", "sz_round", "sz_small", "sz_closed", "sz_capped", "sz_generic"]
+        out["cycles_per_wave"] = {nm: round(dbuf[i] / waves) for i, nm in enumerate(names)}
+        out["cycles_per_wave"]["kernel"] = round(dbuf[13] / waves)
+        out["decisions_per_wave"] = {names[3 + k]: round(dbuf[8 + k] / waves, 1) for k in range(5)}
+        out["cycles_per_decision"] = {names[3 + k]: round(dbuf[3 + k] / max(dbuf[8 + k], 1), 1)
+                                      for k in range(5)}
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
