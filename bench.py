@@ -49,11 +49,11 @@ def parse():
     ap.add_argument("--imhk-steps", type=int, default=16, help="IMHK steps per bench step")
     ap.add_argument("--no-v", action="store_true", help="skip lattice points (coefficients only)")
     ap.add_argument("--exact-order", action="store_true")
-    ap.add_argument("--cpu-samples", type=int, default=1024, help="IMHK proposals for the CPU baseline")
+    ap.add_argument("--cpu-samples", type=int, default=16384, help="IMHK proposals for the CPU baseline")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-csv", default=os.environ.get(
-                        "LGS_TRAFFIC_CSV", os.path.join(REPO, "profiles", "r01_pmc_klein.csv")),
+                        "LGS_TRAFFIC_CSV", os.path.join(REPO, "profiles", "r01f_pmc_klein.csv")),
                     help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE")
     return ap.parse_args()
 
@@ -201,7 +201,7 @@ def main():
     gemm = None
     if g_n:
         # B z over all proposals + the carried states: 2 d^2 flops per vector
-        gemm = {"kernel": "bz_gemm_kernel", "ms_per_step": round(g_ms / args.steps, 3),
+        gemm = {"kernel": "bz_gemm_kernel" if os.environ.get("LGS_BZ_FP64") == "1" else "bz_i8_kernel", "ms_per_step": round(g_ms / args.steps, 3),
                 "tflops": round(2.0 * d * d * (units + nc) * args.steps / (g_ms / 1e3) / 1e12, 2)}
 
     # ---- parity spot check of this run's first proposals against the oracle
