@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <climits>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -114,8 +115,10 @@ struct lgs_ctx {
     int zint = 4;  // internal coefficient store width (bytes); LGS_ZINT=2: 16-bit, sticky 32-bit on overflow
     // timing
     bool timing = false;
-    double t_ms[4] = {0, 0, 0, 0};
-    int64_t t_n[4] = {0, 0, 0, 0};
+    double t_ms[6] = {0, 0, 0, 0, 0, 0};
+    int64_t t_n[6] = {0, 0, 0, 0, 0, 0};
+    // diagnostics scratch (lgs_series_stats / lgs_gram / lgs_jump_distance / lgs_marginal_tvd)
+    DevBuf dg_x, dg_y, dg_out, dg_a, dg_b, dg_c;
     std::vector<Timer> pending;
     std::vector<hipEvent_t> pool;
 };
@@ -1029,7 +1032,7 @@ int lgs_timing_enable(lgs_ctx* c, int enable) {
     int rc = check_ctx(c, false);
     if (rc) return rc;
     c->timing = enable != 0;
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 6; ++k) {
         c->t_ms[k] = 0;
         c->t_n[k] = 0;
     }
@@ -1038,7 +1041,7 @@ int lgs_timing_enable(lgs_ctx* c, int enable) {
 
 int lgs_timing_get(lgs_ctx* c, int kernel, double* ms, int64_t* n) {
     if (!c) return fail(LGS_ERR_INVALID, "null context");
-    if (kernel < 0 || kernel > 3) return fail(LGS_ERR_INVALID, "kernel id 0..3");
+    if (kernel < 0 || kernel > 5) return fail(LGS_ERR_INVALID, "kernel id 0..5");
     if (ms) *ms = c->t_ms[kernel];
     if (n) *n = c->t_n[kernel];
     return LGS_OK;
@@ -1055,6 +1058,268 @@ int lgs_device_info(lgs_ctx* c, char* name, int name_len, int* n_cu, int64_t* hb
     if (n_cu) *n_cu = p.multiProcessorCount;
     if (hbm) *hbm = (int64_t)p.totalGlobalMem;
     return LGS_OK;
+}
+
+}  // extern "C"
+
+// ============================================================ diagnostics
+namespace {
+
+int xtype_of(uint32_t flags, int& xb) {
+    const uint32_t t = flags & (LGS_X_I32 | LGS_X_I64);
+    if (t == (LGS_X_I32 | LGS_X_I64)) return -1;
+    xb = t == LGS_X_I32 ? 4 : 8;
+    return t == LGS_X_I32 ? 1 : t == LGS_X_I64 ? 2 : 0;
+}
+
+// device view of a caller buffer of `bytes` (copied in for host pointers)
+int dev_in(lgs_ctx* c, bool dev, const void* p, size_t bytes, DevBuf& buf, const void*& out) {
+    if (dev) {
+        out = p;
+        return LGS_OK;
+    }
+    int rc = buf.reserve(bytes);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(buf.p, p, bytes, hipMemcpyHostToDevice, c->stream));
+    out = buf.p;
+    return LGS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lgs_series_stats(lgs_ctx* c, const void* x, int64_t n_series, int64_t n, int64_t group_size,
+                     int64_t group_stride, int64_t series_stride, int64_t time_stride,
+                     int64_t max_lag, double window_c, int64_t batch_size, double* mean_out,
+                     double* c0_out, double* acf_out, double* tau_out, double* batch_means_out,
+                     uint32_t flags) {
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    int xb = 8;
+    const int xt = xtype_of(flags, xb);
+    if (xt < 0) return fail(LGS_ERR_INVALID, "LGS_X_I32 and LGS_X_I64 are exclusive");
+    if (n_series < 0 || n < 0 || group_size <= 0 || group_stride < 0 || series_stride < 0 ||
+        time_stride < 0 || batch_size < 0)
+        return fail(LGS_ERR_INVALID, "bad sizes / strides");
+    if (n_series == 0) return LGS_OK;
+    if (n == 0) return fail(LGS_ERR_INVALID, "empty series (the reference divides by len(x) = 0)");
+    if (!x) return fail(LGS_ERR_INVALID, "null x");
+    if ((acf_out || tau_out || c0_out) && max_lag < 0) return fail(LGS_ERR_INVALID, "max_lag < 0");
+    if (batch_means_out && batch_size == 0) return fail(LGS_ERR_INVALID, "batch_size must be > 0");
+    if (xt == 1 && n > (int64_t)1 << 32)
+        return fail(LGS_ERR_INVALID, "int32 series longer than 2^32 (exact int64 sums)");
+    const bool dev = flags & LGS_DEVICE_PTRS;
+    const int64_t L = max_lag < n - 1 ? max_lag : n - 1;
+    const int64_t nlag = L + 1, nb = batch_size ? n / batch_size : 0;
+    const int64_t ng = (n_series + group_size - 1) / group_size;
+    const int64_t last_s = n_series - 1;
+    const size_t span = (size_t)((last_s / group_size) * group_stride + (last_s % group_size) * series_stride +
+                                 (n - 1) * time_stride + 1);
+    (void)ng;
+    const void* X = nullptr;
+    if ((rc = dev_in(c, dev, x, span * xb, c->dg_x, X))) return rc;
+    // outputs: device buffers directly, or one staging block for host pointers
+    const size_t o_mean = 0, o_c0 = n_series, o_tau = 2 * n_series, o_acf = 3 * n_series,
+                 o_bm = o_acf + (acf_out ? (size_t)n_series * nlag : 0),
+                 o_end = o_bm + (batch_means_out ? (size_t)n_series * nb : 0);
+    double* O = nullptr;
+    if (!dev) {
+        if ((rc = c->dg_out.reserve(o_end * 8))) return rc;
+        O = c->dg_out.as<double>();
+    }
+    lgs::SeriesArgs a{};
+    a.x = X;
+    a.xtype = xt;
+    a.n_series = n_series;
+    a.n = n;
+    a.gsize = group_size;
+    a.gstride = group_stride;
+    a.sstride = series_stride;
+    a.tstride = time_stride;
+    a.max_lag = (acf_out || tau_out || c0_out) ? max_lag : -1;
+    a.window_c = window_c;
+    a.batch = batch_means_out ? batch_size : 0;
+    a.mean = mean_out ? (dev ? mean_out : O + o_mean) : nullptr;
+    a.c0 = c0_out ? (dev ? c0_out : O + o_c0) : nullptr;
+    a.tau = tau_out ? (dev ? tau_out : O + o_tau) : nullptr;
+    a.acf = acf_out ? (dev ? acf_out : O + o_acf) : nullptr;
+    a.ld_acf = nlag;
+    a.bmeans = batch_means_out ? (dev ? batch_means_out : O + o_bm) : nullptr;
+    a.ld_b = nb;
+    if ((rc = reset_flags(c))) return rc;
+    {
+        Scope s(c, 5);
+        HIP_TRY(lgs::launch::series_stats(a, c->stream));
+    }
+    if (!dev) {
+        auto back = [&](double* dst, size_t off, size_t cnt) -> int {
+            if (dst) HIP_TRY(hipMemcpyAsync(dst, O + off, cnt * 8, hipMemcpyDeviceToHost, c->stream));
+            return LGS_OK;
+        };
+        if ((rc = back(mean_out, o_mean, n_series)) || (rc = back(c0_out, o_c0, n_series)) ||
+            (rc = back(tau_out, o_tau, n_series)) || (rc = back(acf_out, o_acf, (size_t)n_series * nlag)) ||
+            (rc = back(batch_means_out, o_bm, (size_t)n_series * nb)))
+            return rc;
+    }
+    return finish(c);
+}
+
+int lgs_gram(lgs_ctx* c, int64_t d, int64_t n, const void* x, int64_t ldx, const void* shift,
+             void* sum_out, void* gram_out, uint32_t flags) {
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    int xb = 8;
+    const int xt = xtype_of(flags, xb);
+    if (xt < 0 || d <= 0 || n < 0 || d > (1 << 20)) return fail(LGS_ERR_INVALID, "bad d / n / type");
+    if (!gram_out && !sum_out) return LGS_OK;
+    if (n == 0) return LGS_OK;
+    if (!x) return fail(LGS_ERR_INVALID, "null x");
+    const bool dev = flags & LGS_DEVICE_PTRS, cm = flags & LGS_COORD_MAJOR;
+    if (cm ? ldx < n : ldx != d) return fail(LGS_ERR_INVALID, "ldx: >= n (coordinate-major) or == d (row-major)");
+    if ((rc = reset_flags(c))) return rc;
+    const size_t xbytes = cm ? ((size_t)(d - 1) * ldx + n) * xb : (size_t)n * d * xb;
+    const void* Xin = nullptr;
+    if ((rc = dev_in(c, dev, x, xbytes, c->dg_x, Xin))) return rc;
+    const void* Xc = Xin;
+    int64_t ld = ldx;
+    if (!cm) {  // row-major -> coordinate-major scratch (8-byte elements move as bit patterns)
+        if ((rc = c->dg_y.reserve((size_t)n * d * xb))) return rc;
+        HIP_TRY(lgs::launch::to_coord_major(Xin, xb, n, (int)d, c->dg_y.p, xb, n, c->stream));
+        Xc = c->dg_y.p;
+        ld = n;
+    }
+    const void* SH = nullptr;
+    if (shift && (rc = dev_in(c, dev, shift, (size_t)d * 8, c->dg_c, SH))) return rc;
+    // accumulators: the caller's (device) or staged copies of the host values (ADDED to)
+    void* G = gram_out;
+    void* S = sum_out;
+    const size_t gbytes = (size_t)d * d * 8, sbytes = (size_t)d * 8;
+    if (!dev || !gram_out || !sum_out) {
+        if ((rc = c->dg_a.reserve(gbytes)) || (rc = c->dg_b.reserve(sbytes))) return rc;
+        if (!dev || !gram_out) {
+            G = c->dg_a.p;
+            if (gram_out)
+                HIP_TRY(hipMemcpyAsync(G, gram_out, gbytes, hipMemcpyHostToDevice, c->stream));
+            else
+                HIP_TRY(hipMemsetAsync(G, 0, gbytes, c->stream));
+        }
+        if (!dev || !sum_out) {
+            S = c->dg_b.p;
+            if (sum_out)
+                HIP_TRY(hipMemcpyAsync(S, sum_out, sbytes, hipMemcpyHostToDevice, c->stream));
+            else
+                HIP_TRY(hipMemsetAsync(S, 0, sbytes, c->stream));
+        }
+    }
+    const bool i8 = xt != 0;
+    if (i8) {  // keep the accumulators' prior values for an exact replay
+        if ((rc = c->dg_out.reserve(gbytes + sbytes))) return rc;
+        HIP_TRY(hipMemcpyAsync(c->dg_out.p, G, gbytes, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync((char*)c->dg_out.p + gbytes, S, sbytes, hipMemcpyDeviceToDevice, c->stream));
+    }
+    {
+        Scope s(c, 4);
+        HIP_TRY(lgs::launch::gram(Xc, xt, ld, (int)d, n, i8, SH, G, S, c->flags.as<unsigned int>(),
+                                  c->stream));
+    }
+    if (i8) {
+        unsigned int f = 0;
+        HIP_TRY(hipMemcpyAsync(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (f & lgs::kFlagI8Range) {  // some |x - shift| > 32639: exact int64 VALU replay
+            HIP_TRY(hipMemcpyAsync(G, c->dg_out.p, gbytes, hipMemcpyDeviceToDevice, c->stream));
+            HIP_TRY(hipMemcpyAsync(S, (char*)c->dg_out.p + gbytes, sbytes, hipMemcpyDeviceToDevice, c->stream));
+            Scope s(c, 4);
+            HIP_TRY(lgs::launch::gram(Xc, xt, ld, (int)d, n, false, SH, G, S, nullptr, c->stream));
+        }
+        HIP_TRY(hipMemsetAsync(c->flags.p, 0, 16, c->stream));
+    }
+    if (!dev) {
+        if (gram_out) HIP_TRY(hipMemcpyAsync(gram_out, G, gbytes, hipMemcpyDeviceToHost, c->stream));
+        if (sum_out) HIP_TRY(hipMemcpyAsync(sum_out, S, sbytes, hipMemcpyDeviceToHost, c->stream));
+    }
+    return finish(c);
+}
+
+int lgs_jump_distance(lgs_ctx* c, int64_t n, int64_t d, const void* x, int64_t ld, double* out,
+                      uint32_t flags) {
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    int xb = 8;
+    const int xt = xtype_of(flags, xb);
+    if (xt < 0 || n < 0 || d <= 0 || ld < d) return fail(LGS_ERR_INVALID, "bad arguments");
+    if (n < 2) return LGS_OK;
+    if (!x || !out) return fail(LGS_ERR_INVALID, "null buffer");
+    const bool dev = flags & LGS_DEVICE_PTRS;
+    if ((rc = reset_flags(c))) return rc;
+    const void* X = nullptr;
+    if ((rc = dev_in(c, dev, x, ((size_t)(n - 1) * ld + d) * xb, c->dg_x, X))) return rc;
+    double* O = out;
+    if (!dev) {
+        if ((rc = c->dg_out.reserve((size_t)(n - 1) * 8))) return rc;
+        O = c->dg_out.as<double>();
+    }
+    HIP_TRY(lgs::launch::jump(X, xt, n, (int)d, ld, O, c->stream));
+    if (!dev) HIP_TRY(hipMemcpyAsync(out, O, (size_t)(n - 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    return finish(c);
+}
+
+int lgs_marginal_tvd(lgs_ctx* c, int64_t d, const void* x1, int64_t n1, const void* x2, int64_t n2,
+                     double* tvd_out, uint32_t flags) {
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    int xb = 8;
+    const int xt = xtype_of(flags, xb);
+    if (xt < 0 || d <= 0 || n1 <= 0 || n2 <= 0) return fail(LGS_ERR_INVALID, "bad arguments");
+    if (!x1 || !x2 || !tvd_out) return fail(LGS_ERR_INVALID, "null buffer");
+    const bool dev = flags & LGS_DEVICE_PTRS;
+    if ((rc = reset_flags(c))) return rc;
+    const void *X1 = nullptr, *X2 = nullptr;
+    if ((rc = dev_in(c, dev, x1, (size_t)n1 * d * xb, c->dg_x, X1)) ||
+        (rc = dev_in(c, dev, x2, (size_t)n2 * d * xb, c->dg_y, X2)))
+        return rc;
+    // per-coordinate value range over both sets
+    if ((rc = c->dg_a.reserve((size_t)(3 * d + 1) * 8))) return rc;
+    long long* mn = c->dg_a.as<long long>();
+    long long* mx = mn + d;
+    long long* off = mx + d;
+    std::vector<long long> h_mn(d, LLONG_MAX), h_mx(d, LLONG_MIN), h_off(d + 1, 0);
+    HIP_TRY(hipMemcpyAsync(mn, h_mn.data(), d * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(mx, h_mx.data(), d * 8, hipMemcpyHostToDevice, c->stream));
+    unsigned int* fl = c->flags.as<unsigned int>();
+    HIP_TRY(lgs::launch::tvd_minmax(X1, xt, n1, (int)d, mn, mx, fl, c->stream));
+    HIP_TRY(lgs::launch::tvd_minmax(X2, xt, n2, (int)d, mn, mx, fl, c->stream));
+    unsigned int f = 0;
+    HIP_TRY(hipMemcpyAsync(h_mn.data(), mn, d * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(h_mx.data(), mx, d * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&f, fl, sizeof(f), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (f & lgs::kFlagNonFinite)
+        return fail(LGS_ERR_INVALID, "marginal TVD: samples must be integer-valued (discrete case)");
+    const long long kMaxBins = 1LL << 28;
+    for (int64_t i = 0; i < d; ++i) {
+        const long long w = h_mx[i] - h_mn[i] + 1;
+        if (w <= 0 || w > kMaxBins || h_off[i] + w > kMaxBins)
+            return fail(LGS_ERR_INVALID, "marginal TVD: value ranges exceed 2^28 bins in total");
+        h_off[i + 1] = h_off[i] + w;
+    }
+    const long long bins = h_off[d];
+    HIP_TRY(hipMemcpyAsync(off, h_off.data(), (d + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    if ((rc = c->dg_b.reserve((size_t)bins * 8))) return rc;
+    unsigned int* c1 = c->dg_b.as<unsigned int>();
+    unsigned int* c2 = c1 + bins;
+    HIP_TRY(hipMemsetAsync(c1, 0, (size_t)bins * 8, c->stream));
+    HIP_TRY(lgs::launch::tvd_hist(X1, xt, n1, (int)d, mn, off, c1, c->stream));
+    HIP_TRY(lgs::launch::tvd_hist(X2, xt, n2, (int)d, mn, off, c2, c->stream));
+    double* O = tvd_out;
+    if (!dev) {
+        if ((rc = c->dg_out.reserve((size_t)d * 8))) return rc;
+        O = c->dg_out.as<double>();
+    }
+    HIP_TRY(lgs::launch::tvd_sum(c1, c2, off, (int)d, n1, n2, O, c->stream));
+    if (!dev) HIP_TRY(hipMemcpyAsync(tvd_out, O, (size_t)d * 8, hipMemcpyDeviceToHost, c->stream));
+    return finish(c);
 }
 
 }  // extern "C"

@@ -1,0 +1,541 @@
+// lgs_diag.hip -- diagnostics on the sample stream, gfx950.
+//
+//   series_stats_kernel  per scalar series: mean, lag-k autocovariance / ACF
+//                        (mcmc_diag.py:12-33, convergence_diag.py:75-113), the
+//                        Sokal-windowed integrated autocorrelation time
+//                        (mcmc_diag.py:36-56, convergence_diag.py:116-145) with an
+//                        early exit once the window closes, and batch means
+//                        (mcmc_diag.py:79-98, 228-241; convergence_diag.py:316-345).
+//   gram_i8_kernel       exact integer second moments  sum_s z z^T  and  sum_s z of
+//                        coefficient vectors (empirical mean / covariance,
+//                        base.py:154-160) on v_mfma_i32_32x32x32_i8 with two balanced
+//                        base-256 digits per coefficient; gram_val_kernel is the exact
+//                        int64 VALU replay for |z| > 32639 and the fp64 path for
+//                        real-valued samples (centred on their mean, as np.cov).
+//   jump_kernel          ||x_{t+1} - x_t||_2 (mcmc_diag.py:120-136).
+//   tvd_* kernels        discrete marginal total-variation distance between two
+//                        sample sets (convergence_diag.py:15-48, 66-72).
+//
+// Series layout: series s starts at (s / gsize) * gstride + (s % gsize) * sstride
+// elements and advances by tstride per time step, so a row-major (n x d) sample
+// matrix (one series per coordinate), a chain-major IMHK trace (chains x steps x d)
+// or a coordinate-major store are all read in place.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "lgs_kernels.h"
+
+namespace lgs {
+
+namespace {
+
+template <typename XT>
+__device__ __forceinline__ double as_f64(XT v) {
+    return (double)v;
+}
+
+// exact integer sum (long long) or fp64 sum, as the element type allows
+template <typename XT>
+struct SumT {
+    using T = long long;
+};
+template <>
+struct SumT<double> {
+    using T = double;
+};
+
+template <typename T>
+__device__ T block_sum(T v, T* sh) {  // 256 threads, fixed tree order
+    const int tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) sh[tid] += sh[tid + o];
+        __syncthreads();
+    }
+    const T r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ per-series statistics
+// One workgroup (256 threads) per series.  Lags are processed in blocks of 64
+// (16 lag quads x 16 time slices per pass); the time axis is staged through LDS
+// in chunks of 4096 mean-centred values (left factor) plus the lag-shifted window
+// (right factor), each thread sliding a 4-lag register window along its slice:
+// 2 LDS reads per 4 FMAs.  Values past the end are staged as 0, so the pair
+// (t, t+k) contributes only while t + k < n, exactly the 'full' correlation.
+constexpr int kAcfCH = 4096, kAcfLB = 64;
+
+template <typename XT>
+__global__ __launch_bounds__(256) void series_stats_kernel(SeriesArgs a) {
+    __shared__ double Ls[kAcfCH];
+    __shared__ double Rs[kAcfCH + kAcfLB];
+    __shared__ double red[16][kAcfLB];
+    __shared__ double gam[kAcfLB];
+    __shared__ typename SumT<XT>::T sred[256];
+    __shared__ int sh_stop;
+    const int tid = threadIdx.x;
+    const int64_t s = (int64_t)blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+    if (s >= a.n_series) return;
+    const XT* x = (const XT*)a.x + (s / a.gsize) * a.gstride + (s % a.gsize) * a.sstride;
+    const int64_t n = a.n, ts = a.tstride;
+
+    // mean (np.mean: exact for integer-valued data while |sum| < 2^53)
+    typename SumT<XT>::T part = 0;
+    for (int64_t t = tid; t < n; t += 256) part += x[t * ts];
+    const double mean = (double)block_sum(part, sred) / (double)n;
+    if (tid == 0 && a.mean) a.mean[s] = mean;
+
+    // batch means: mean of x[j*b : (j+1)*b], j < n // b
+    if (a.batch > 0 && a.bmeans) {
+        const int64_t nb = n / a.batch;
+        for (int64_t j = tid; j < nb; j += 256) {
+            typename SumT<XT>::T bs = 0;
+            for (int64_t t = j * a.batch; t < (j + 1) * a.batch; ++t) bs += x[t * ts];
+            a.bmeans[s * a.ld_b + j] = (double)bs / (double)a.batch;
+        }
+    }
+    if (a.max_lag < 0) return;
+
+    const int64_t L = a.max_lag < n - 1 ? a.max_lag : n - 1;
+    const int q = tid & 15, sl = tid >> 4;
+    const int tb = sl * (kAcfCH / 16);
+    double c0 = 0.0, tau = 0.0;  // thread 0's running state
+    int stopped = 0;
+    if (tid == 0) sh_stop = 0;
+    for (int64_t kb = 0; kb <= L; kb += kAcfLB) {
+        double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
+        for (int64_t t0 = 0; t0 < n - kb; t0 += kAcfCH) {
+            __syncthreads();
+            for (int i = tid; i < kAcfCH; i += 256) {
+                const int64_t t = t0 + i;
+                Ls[i] = t < n ? as_f64(x[t * ts]) - mean : 0.0;
+            }
+            for (int i = tid; i < kAcfCH + kAcfLB; i += 256) {
+                const int64_t t = t0 + kb + i;
+                Rs[i] = t < n ? as_f64(x[t * ts]) - mean : 0.0;
+            }
+            __syncthreads();
+            const double* rp = Rs + tb + 4 * q;
+            double w0 = rp[0], w1 = rp[1], w2 = rp[2], w3 = rp[3];
+#pragma unroll 8
+            for (int tt = 0; tt < kAcfCH / 16; ++tt) {
+                const double yl = Ls[tb + tt];
+                acc0 += yl * w0;
+                acc1 += yl * w1;
+                acc2 += yl * w2;
+                acc3 += yl * w3;
+                w0 = w1;
+                w1 = w2;
+                w2 = w3;
+                w3 = rp[tt + 4];
+            }
+        }
+        red[sl][4 * q + 0] = acc0;
+        red[sl][4 * q + 1] = acc1;
+        red[sl][4 * q + 2] = acc2;
+        red[sl][4 * q + 3] = acc3;
+        __syncthreads();
+        if (tid < kAcfLB) {
+            double g = 0.0;
+            for (int j = 0; j < 16; ++j) g += red[j][tid];
+            gam[tid] = g;
+        }
+        __syncthreads();
+        const double c0b = kb == 0 ? gam[0] : 0.0;
+        if (kb == 0 && tid == 0 && a.c0) a.c0[s] = c0b;
+        if (tid == 0) {
+            if (kb == 0) c0 = c0b;
+            for (int l = 0; l < kAcfLB && kb + l <= L; ++l) {
+                const int64_t k = kb + l;
+                const double r = gam[l] / c0;
+                if (a.acf) a.acf[s * a.ld_acf + k] = r;
+                if (k >= 1 && !stopped) {  // tau_int += 2 acf[k]; stop once k >= c tau_int
+                    tau += 2.0 * r;
+                    if ((double)k >= a.window_c * tau) stopped = 1;
+                }
+            }
+            sh_stop = stopped && !a.acf;
+        }
+        __syncthreads();
+        if (sh_stop) break;
+    }
+    if (tid == 0 && a.tau) a.tau[s] = 1.0 + tau;
+}
+
+// ------------------------------------------------------------ exact sum z z^T
+// Block tile 128 x 128 of the d x d Gram matrix (upper tile pairs only; the
+// mirrored entries are written too), K = samples split over blockIdx.y in chunks of
+// kc <= 32768 so the int32 digit-class sums stay exact (2 kc 2^14 < 2^31).
+// 8 waves as 2 x 4, each 64 x 32 = two 32x32 MFMA tiles; K steps of 64 samples
+// through LDS as balanced base-256 digit planes [coord][sample] (pitch 80 bytes).
+//   z z' = 65536 h h' + 256 (h l' + l h') + l l'
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v16i_t __attribute__((ext_vector_type(16)));
+
+template <typename ZT>
+__device__ __forceinline__ void gram_stage(const ZT* __restrict__ Z, int64_t ldz, int d, int64_t k,
+                                           int64_t k1, int r0, int tid, int8_t* D1, int8_t* D0,
+                                           const long long* __restrict__ shift, bool& bad,
+                                           long long* zsum) {
+    constexpr int P = 80;
+    const int row = tid >> 2, part = tid & 3;
+    const int gr = r0 + row;
+    const int64_t kk = k + part * 16;
+    const ZT* zp = Z + (size_t)gr * ldz + kk;
+    const bool rok = gr < d;
+    const long long sh = (rok && shift) ? shift[gr] : 0;
+    v4i_t w0, w1;
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+        unsigned int lo4 = 0, hi4 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = qd * 4 + j;
+            const long long zr = (rok && kk + e < k1) ? (long long)zp[e] - sh : 0;
+            bad |= (zr > 32639) | (zr < -32639);
+            const int z = (int)zr;
+            if (zsum) *zsum += zr;
+            const int lo = (z << 24) >> 24;
+            const int hi = (z - lo) >> 8;
+            lo4 |= ((unsigned int)lo & 0xffu) << (8 * j);
+            hi4 |= ((unsigned int)hi & 0xffu) << (8 * j);
+        }
+        w0[qd] = (int)lo4;
+        w1[qd] = (int)hi4;
+    }
+    *(v4i_t*)&D0[row * P + part * 16] = w0;
+    *(v4i_t*)&D1[row * P + part * 16] = w1;
+}
+
+__device__ __forceinline__ void atomic_add_val(long long* p, long long v) {
+    atomicAdd((unsigned long long*)p, (unsigned long long)v);
+}
+__device__ __forceinline__ void atomic_add_val(double* p, double v) { atomicAdd(p, v); }
+
+__device__ __forceinline__ void tile_pair(int p, int nt, int& ti, int& tj) {
+    int i = 0;
+    while (p >= nt - i) {
+        p -= nt - i;
+        ++i;
+    }
+    ti = i;
+    tj = i + p;
+}
+
+template <typename ZT>
+__global__ __launch_bounds__(512) void gram_i8_kernel(const ZT* __restrict__ Z, int64_t ldz, int d,
+                                                      int64_t n, int64_t kc, int nt,
+                                                      const long long* __restrict__ shift,
+                                                      unsigned long long* __restrict__ G,
+                                                      unsigned long long* __restrict__ S,
+                                                      unsigned int* flags) {
+    constexpr int BT = 128, KC = 64, P = 80;
+    __shared__ __attribute__((aligned(16))) int8_t A1[BT * P], A0[BT * P], B1[BT * P], B0[BT * P];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    int ti, tj;
+    tile_pair((int)blockIdx.x, nt, ti, tj);
+    const bool diag = ti == tj;
+    const int64_t k0 = (int64_t)blockIdx.y * kc;
+    const int64_t k1 = k0 + kc < n ? k0 + kc : n;
+    v16i_t h[2], m[2], l[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        h[t] = (v16i_t){};
+        m[t] = (v16i_t){};
+        l[t] = (v16i_t){};
+    }
+    bool bad = false;
+    long long zsum = 0;
+    const int8_t* Bh = diag ? A1 : B1;
+    const int8_t* Bl = diag ? A0 : B0;
+    for (int64_t k = k0; k < k1; k += KC) {
+        gram_stage<ZT>(Z, ldz, d, k, k1, ti * BT, tid, A1, A0, shift, bad, diag ? &zsum : nullptr);
+        if (!diag) gram_stage<ZT>(Z, ldz, d, k, k1, tj * BT, tid, B1, B0, shift, bad, nullptr);
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int kb = ks * 32 + 16 * (lane >> 5);
+            const int col = wn * 32 + (lane & 31);
+            const v4i_t b1 = *(const v4i_t*)&Bh[col * P + kb];
+            const v4i_t b0 = *(const v4i_t*)&Bl[col * P + kb];
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+                const int arow = wm * 64 + rt * 32 + (lane & 31);
+                const v4i_t a1 = *(const v4i_t*)&A1[arow * P + kb];
+                const v4i_t a0 = *(const v4i_t*)&A0[arow * P + kb];
+                h[rt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, h[rt], 0, 0, 0);
+                m[rt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, m[rt], 0, 0, 0);
+                m[rt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, m[rt], 0, 0, 0);
+                l[rt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, l[rt], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int gi = ti * BT + wm * 64 + rt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+            const int gj = tj * BT + wn * 32 + (lane & 31);
+            if (gi < d && gj < d) {
+                const long long v = 65536LL * h[rt][reg] + 256LL * m[rt][reg] + (long long)l[rt][reg];
+                if (v) {
+                    atomicAdd(G + (size_t)gi * d + gj, (unsigned long long)v);
+                    if (!diag) atomicAdd(G + (size_t)gj * d + gi, (unsigned long long)v);
+                }
+            }
+        }
+    if (diag && S && zsum) atomicAdd(S + ti * BT + (tid >> 2), (unsigned long long)zsum);
+    if (bad) atomicOr(flags, kFlagI8Range);
+}
+
+// VALU Gram: exact int64 replay for integer data (any |z - shift| < 2^31 with sums
+// below 2^63), or fp64 for real-valued samples (shift = their mean, so the
+// products are centred as in np.cov).  64 x 64 output tiles, 256 threads with 4 x 4
+// outputs each, samples staged 16 at a time.
+template <typename ZT, typename AT>
+__global__ __launch_bounds__(256) void gram_val_kernel(const ZT* __restrict__ Z, int64_t ldz, int d,
+                                                       int64_t n, int64_t kc, int nt,
+                                                       const AT* __restrict__ shift, AT* __restrict__ G,
+                                                       AT* __restrict__ S) {
+    constexpr int BT = 64, KS = 16;
+    __shared__ AT As[KS][BT + 1], Bs[KS][BT + 1];
+    const int tid = threadIdx.x;
+    int ti, tj;
+    tile_pair((int)blockIdx.x, nt, ti, tj);
+    const bool diag = ti == tj;
+    const int64_t k0 = (int64_t)blockIdx.y * kc;
+    const int64_t k1 = k0 + kc < n ? k0 + kc : n;
+    const int tr = (tid >> 4) * 4, tc = (tid & 15) * 4;
+    AT acc[4][4] = {};
+    AT zsum = 0;
+    for (int64_t k = k0; k < k1; k += KS) {
+        for (int e = tid; e < KS * BT; e += 256) {
+            const int r = e / KS, kk = e % KS;
+            const int gi = ti * BT + r, gj = tj * BT + r;
+            const bool kok = k + kk < k1;
+            As[kk][r] = (gi < d && kok) ? (AT)Z[(size_t)gi * ldz + k + kk] - (shift ? shift[gi] : (AT)0) : (AT)0;
+            Bs[kk][r] = (gj < d && kok) ? (AT)Z[(size_t)gj * ldz + k + kk] - (shift ? shift[gj] : (AT)0) : (AT)0;
+        }
+        __syncthreads();
+        if (diag && tid < BT)
+            for (int kk = 0; kk < KS; ++kk) zsum += As[kk][tid];
+#pragma unroll 4
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] += As[kk][tr + i] * Bs[kk][tc + j];
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int gi = ti * BT + tr + i, gj = tj * BT + tc + j;
+            if (gi < d && gj < d && acc[i][j] != (AT)0) {
+                atomic_add_val(G + (size_t)gi * d + gj, acc[i][j]);
+                if (!diag) atomic_add_val(G + (size_t)gj * d + gi, acc[i][j]);
+            }
+        }
+    if (diag && S && tid < BT && ti * BT + tid < d && zsum != (AT)0) atomic_add_val(S + ti * BT + tid, zsum);
+}
+
+// ------------------------------------------------------------ jump distances
+// One wave per step t: lanes over the d coordinates of rows t and t+1.
+template <typename XT>
+__global__ __launch_bounds__(256) void jump_kernel(const XT* __restrict__ x, int64_t n, int d,
+                                                   int64_t ld, double* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t + 1 >= n) return;
+    const XT* r0 = x + (size_t)t * ld;
+    const XT* r1 = r0 + ld;
+    double acc = 0.0;
+    for (int i = lane; i < d; i += 64) {
+        const double df = as_f64(r1[i]) - as_f64(r0[i]);
+        acc += df * df;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) out[t] = sqrt(acc);
+}
+
+// ------------------------------------------------------------ discrete marginal TVD
+// Pass 1: per-coordinate min / max over both sets (integer-valued data; a
+// non-integral fp64 value sets kFlagNonFinite).  Pass 2: per-coordinate counts in
+// global memory (bins [min_i, max_i]).  Pass 3: one thread per coordinate sums
+// |c1/n1 - c2/n2| over its bins in ascending value order -- the order of the
+// reference's loop over np.unique (convergence_diag.py:35-46), so the result is
+// bit-identical.
+template <typename XT>
+__device__ __forceinline__ bool to_i64(XT v, long long& o) {
+    o = (long long)v;
+    return true;
+}
+template <>
+__device__ __forceinline__ bool to_i64<double>(double v, long long& o) {
+    if (!(fabs(v) < 4.0e18) || v != rint(v)) return false;
+    o = (long long)v;
+    return true;
+}
+
+template <typename XT>
+__global__ __launch_bounds__(256) void tvd_minmax_kernel(const XT* __restrict__ x, int64_t n, int d,
+                                                         int64_t rows_per_block, long long* mn,
+                                                         long long* mx, unsigned int* flags) {
+    const int i = blockIdx.y * 256 + threadIdx.x;
+    if (i >= d) return;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+    long long lo = 0x7fffffffffffffffLL, hi = -0x7fffffffffffffffLL - 1;
+    bool bad = false;
+    for (int64_t r = r0; r < r1; ++r) {
+        long long v;
+        if (!to_i64<XT>(x[(size_t)r * d + i], v)) {
+            bad = true;
+            continue;
+        }
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+    if (r1 > r0) {
+        atomicMin(mn + i, lo);
+        atomicMax(mx + i, hi);
+    }
+    if (bad) atomicOr(flags, kFlagNonFinite);
+}
+
+template <typename XT>
+__global__ __launch_bounds__(256) void tvd_hist_kernel(const XT* __restrict__ x, int64_t n, int d,
+                                                       int64_t rows_per_block, const long long* mn,
+                                                       const long long* off, unsigned int* cnt) {
+    const int i = blockIdx.y * 256 + threadIdx.x;
+    if (i >= d) return;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+    const long long base = off[i] - mn[i];
+    for (int64_t r = r0; r < r1; ++r) {
+        long long v;
+        if (to_i64<XT>(x[(size_t)r * d + i], v)) atomicAdd(cnt + base + v, 1u);
+    }
+}
+
+__global__ __launch_bounds__(256) void tvd_sum_kernel(const unsigned int* __restrict__ c1,
+                                                      const unsigned int* __restrict__ c2,
+                                                      const long long* __restrict__ off, int d,
+                                                      double n1, double n2, double* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= d) return;
+    double acc = 0.0;
+    for (long long b = off[i]; b < off[i + 1]; ++b) {
+        const unsigned int a = c1[b], c = c2[b];
+        if (a | c) acc += fabs((double)a / n1 - (double)c / n2);
+    }
+    out[i] = 0.5 * acc;
+}
+
+// ============================================================ launchers
+namespace launch {
+
+#define LGS_XT(xt, T, ...)       \
+    do {                         \
+        if ((xt) == 1) {         \
+            using T = int32_t;   \
+            __VA_ARGS__;         \
+        } else if ((xt) == 2) {  \
+            using T = int64_t;   \
+            __VA_ARGS__;         \
+        } else {                 \
+            using T = double;    \
+            __VA_ARGS__;         \
+        }                        \
+    } while (0)
+
+hipError_t series_stats(const SeriesArgs& a, hipStream_t st) {
+    if (a.n_series <= 0 || a.n <= 0) return hipSuccess;
+    const int64_t gx = a.n_series < 65536 ? a.n_series : 65536;
+    const dim3 grid((unsigned)gx, (unsigned)((a.n_series + gx - 1) / gx));
+    LGS_XT(a.xtype, XT, hipLaunchKernelGGL(series_stats_kernel<XT>, grid, dim3(256), 0, st, a));
+    return hipGetLastError();
+}
+
+int64_t gram_chunk(int64_t n, int nt) {
+    const int64_t pairs = (int64_t)nt * (nt + 1) / 2;
+    int64_t splits = (2048 + pairs - 1) / pairs;
+    int64_t kc = (n + splits - 1) / splits;
+    kc = (kc + 63) / 64 * 64;
+    if (kc < 1024) kc = 1024;
+    if (kc > 32768) kc = 32768;
+    return kc;
+}
+
+hipError_t gram(const void* Z, int xtype, int64_t ldz, int d, int64_t n, bool i8, const void* shift,
+                void* G, void* S, unsigned int* flags, hipStream_t st) {
+    if (n <= 0 || d <= 0) return hipSuccess;
+    if (i8 && xtype != 0) {
+        const int nt = (d + 127) / 128;
+        const int64_t kc = gram_chunk(n, nt);
+        const dim3 grid((unsigned)(nt * (nt + 1) / 2), (unsigned)((n + kc - 1) / kc));
+        auto g = (unsigned long long*)G;
+        auto sm = (unsigned long long*)S;
+        auto sh = (const long long*)shift;
+        if (xtype == 2)
+            hipLaunchKernelGGL(gram_i8_kernel<int64_t>, grid, dim3(512), 0, st, (const int64_t*)Z, ldz, d, n, kc, nt, sh, g, sm, flags);
+        else
+            hipLaunchKernelGGL(gram_i8_kernel<int32_t>, grid, dim3(512), 0, st, (const int32_t*)Z, ldz, d, n, kc, nt, sh, g, sm, flags);
+    } else {
+        const int nt = (d + 63) / 64;
+        const int64_t kc = gram_chunk(n, nt);
+        const dim3 grid((unsigned)(nt * (nt + 1) / 2), (unsigned)((n + kc - 1) / kc));
+        if (xtype == 2)
+            hipLaunchKernelGGL((gram_val_kernel<int64_t, long long>), grid, dim3(256), 0, st, (const int64_t*)Z, ldz, d, n, kc, nt, (const long long*)shift, (long long*)G, (long long*)S);
+        else if (xtype == 1)
+            hipLaunchKernelGGL((gram_val_kernel<int32_t, long long>), grid, dim3(256), 0, st, (const int32_t*)Z, ldz, d, n, kc, nt, (const long long*)shift, (long long*)G, (long long*)S);
+        else
+            hipLaunchKernelGGL((gram_val_kernel<double, double>), grid, dim3(256), 0, st, (const double*)Z, ldz, d, n, kc, nt, (const double*)shift, (double*)G, (double*)S);
+    }
+    return hipGetLastError();
+}
+
+hipError_t jump(const void* x, int xtype, int64_t n, int d, int64_t ld, double* out, hipStream_t st) {
+    if (n < 2) return hipSuccess;
+    const dim3 grid((unsigned)((n - 1 + 3) / 4));
+    LGS_XT(xtype, XT, hipLaunchKernelGGL(jump_kernel<XT>, grid, dim3(256), 0, st, (const XT*)x, n, d, ld, out));
+    return hipGetLastError();
+}
+
+static int64_t tvd_rows(int64_t n) { return n < 256 ? 1 : (n + 1023) / 1024 < 64 ? 64 : (n + 1023) / 1024; }
+
+hipError_t tvd_minmax(const void* x, int xtype, int64_t n, int d, long long* mn, long long* mx,
+                      unsigned int* flags, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t rpb = tvd_rows(n);
+    const dim3 grid((unsigned)((n + rpb - 1) / rpb), (unsigned)((d + 255) / 256));
+    LGS_XT(xtype, XT, hipLaunchKernelGGL(tvd_minmax_kernel<XT>, grid, dim3(256), 0, st, (const XT*)x, n, d, rpb, mn, mx, flags));
+    return hipGetLastError();
+}
+
+hipError_t tvd_hist(const void* x, int xtype, int64_t n, int d, const long long* mn,
+                    const long long* off, unsigned int* cnt, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t rpb = tvd_rows(n);
+    const dim3 grid((unsigned)((n + rpb - 1) / rpb), (unsigned)((d + 255) / 256));
+    LGS_XT(xtype, XT, hipLaunchKernelGGL(tvd_hist_kernel<XT>, grid, dim3(256), 0, st, (const XT*)x, n, d, rpb, mn, off, cnt));
+    return hipGetLastError();
+}
+
+hipError_t tvd_sum(const unsigned int* c1, const unsigned int* c2, const long long* off, int d,
+                   int64_t n1, int64_t n2, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(tvd_sum_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, st, c1, c2, off, d,
+                       (double)n1, (double)n2, out);
+    return hipGetLastError();
+}
+
+}  // namespace launch
+}  // namespace lgs

@@ -113,7 +113,43 @@ struct AcceptArgs {
     int64_t carry_col;   // >= 0: sel of a state carried in from before the block = carry_col + chain
 };
 
+// Per-series statistics (lgs_diag.hip series_stats_kernel).  Series s starts at
+// x + (s / gsize) * gstride + (s % gsize) * sstride, time step t at + t * tstride.
+struct SeriesArgs {
+    const void* x;
+    int xtype;  // 0 fp64, 1 int32, 2 int64
+    int64_t n_series, n, gsize, gstride, sstride, tstride;
+    int64_t max_lag;  // < 0: mean / batch means only
+    double window_c;  // Sokal window constant of the tau_int loop
+    int64_t batch;    // > 0: batch means of this size
+    double* mean;     // nullable, n_series
+    double* c0;       // nullable, n_series: sum (x - mean)^2
+    double* acf;      // nullable, n_series x ld_acf (lags 0..min(max_lag, n-1));
+                      // null with tau set: lag blocks stop once the window closes
+    int64_t ld_acf;
+    double* tau;      // nullable, n_series
+    double* bmeans;   // nullable, n_series x ld_b
+    int64_t ld_b;
+};
+
 namespace launch {
+// ---- diagnostics (lgs_diag.hip); xtype 0 fp64, 1 int32, 2 int64
+hipError_t series_stats(const SeriesArgs& a, hipStream_t st);
+// sum y y^T (d x d, both triangles) and sum y (d), y = x - shift (shift nullable),
+// ADDED to G / S: int64 for integer x (xtype 1 int32, 2 int64; shift int64), fp64
+// for xtype 0 (shift fp64).  x coordinate-major (d x n, ld ldz).
+// i8 (integer x): int8-digit MFMA path, sets kFlagI8Range when |y| > 32639 (redo
+// with i8 = false: exact int64 VALU)
+hipError_t gram(const void* Z, int xtype, int64_t ldz, int d, int64_t n, bool i8, const void* shift,
+                void* G, void* S, unsigned int* flags, hipStream_t st);
+hipError_t jump(const void* x, int xtype, int64_t n, int d, int64_t ld, double* out, hipStream_t st);
+hipError_t tvd_minmax(const void* x, int xtype, int64_t n, int d, long long* mn, long long* mx,
+                      unsigned int* flags, hipStream_t st);
+hipError_t tvd_hist(const void* x, int xtype, int64_t n, int d, const long long* mn,
+                    const long long* off, unsigned int* cnt, hipStream_t st);
+hipError_t tvd_sum(const unsigned int* c1, const unsigned int* c2, const long long* off, int d,
+                   int64_t n1, int64_t n2, double* out, hipStream_t st);
+
 // zb / ob / ib: coefficient element width in bytes (2, 4 or 8)
 hipError_t klein(const KleinArgs& a, const double* R, const double* RP, const double* RC,
                  int panel, int kernel, bool wl, int zb, void* Z, hipStream_t st);

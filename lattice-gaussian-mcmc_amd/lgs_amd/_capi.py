@@ -32,12 +32,17 @@ LGS_SAMPLEZ_TABLE = 0x20
 LGS_SAMPLEZ_DECISION = 0x40
 LGS_SAMPLEZ_LIBM = 0x80
 
+LGS_X_I32 = 0x100
+LGS_X_I64 = 0x200
+
 KERNEL_KLEIN, KERNEL_BZ, KERNEL_ACCEPT, KERNEL_MOMENTS = 0, 1, 2, 3
+KERNEL_GRAM, KERNEL_SERIES = 4, 5
 
 # every symbol include/lgs.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_destroy", "lgs_set_stream",
            "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_lattice_points", "lgs_log_density", "lgs_sample_z", "lgs_timing_enable",
-           "lgs_timing_get", "lgs_device_info")
+           "lgs_timing_get", "lgs_device_info", "lgs_series_stats", "lgs_gram",
+           "lgs_jump_distance", "lgs_marginal_tvd")
 
 
 class LgsError(RuntimeError):
@@ -90,6 +95,12 @@ def load_library(path: str = LIB_PATH):
     L.lgs_timing_get.argtypes = [_vp, ctypes.c_int, _dp, _i64p]
     L.lgs_device_info.argtypes = [_vp, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                   _i64p]
+    _i64 = ctypes.c_int64
+    L.lgs_series_stats.argtypes = [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
+                                   ctypes.c_double, _i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32]
+    L.lgs_gram.argtypes = [_vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp, ctypes.c_uint32]
+    L.lgs_jump_distance.argtypes = [_vp, _i64, _i64, _vp, _i64, _vp, ctypes.c_uint32]
+    L.lgs_marginal_tvd.argtypes = [_vp, _i64, _vp, _i64, _vp, _i64, _vp, ctypes.c_uint32]
     for name in EXPORTS:
         if name not in ("lgs_version", "lgs_last_error"):
             getattr(L, name).restype = ctypes.c_int
@@ -116,6 +127,22 @@ def _ptr(a):
     if isinstance(a, int):
         return ctypes.c_void_p(a)
     raise TypeError(f"unsupported buffer {type(a)}")
+
+
+def _dtype_name(a):
+    return str(a.dtype).replace("torch.", "")
+
+
+def x_flags(a) -> int:
+    """LGS_X_* element-type flag of a host array / device tensor (fp64, int32, int64)."""
+    t = _dtype_name(a)
+    if t == "float64":
+        return 0
+    if t == "int32":
+        return LGS_X_I32
+    if t == "int64":
+        return LGS_X_I64
+    raise TypeError(f"diagnostics take float64 / int32 / int64 data, got {t}")
 
 
 class Context:
@@ -220,6 +247,41 @@ class Context:
         _check(_lib.lgs_sample_z(self._h, mu.size, _ptr(mu), _ptr(sg), _ptr(uu), int(precision),
                                  _ptr(z), _ptr(ln), f))
         return z, ln
+
+    # ---------------------------------------------------------------- diagnostics
+    def series_stats(self, x, n_series, n, group_size, group_stride, series_stride, time_stride,
+                     max_lag=-1, window_c=5.0, batch_size=0, mean=None, c0=None, acf=None,
+                     tau=None, batch_means=None, flags=0):
+        """Raw lgs_series_stats; x / outputs are host arrays or device tensors
+        (flags must then carry LGS_DEVICE_PTRS); element type via x_flags(x)."""
+        _check(_lib.lgs_series_stats(self._h, _ptr(x), int(n_series), int(n), int(group_size),
+                                     int(group_stride), int(series_stride), int(time_stride),
+                                     int(max_lag), float(window_c), int(batch_size), _ptr(mean),
+                                     _ptr(c0), _ptr(acf), _ptr(tau), _ptr(batch_means),
+                                     int(flags | x_flags(x))))
+
+    def gram(self, x, shift=None, sum_out=None, gram_out=None, coord_major=False, flags=0):
+        """sum y and sum y y^T, y = x - shift, ADDED to sum_out (d) / gram_out (d x d):
+        int64 (exact) for int32 / int64 x, fp64 for float64 x."""
+        f = flags | (LGS_COORD_MAJOR if coord_major else 0) | x_flags(x)
+        if coord_major:
+            d, n = x.shape
+        else:
+            n, d = x.shape
+        _check(_lib.lgs_gram(self._h, int(d), int(n), _ptr(x), int(n if coord_major else d),
+                             _ptr(shift), _ptr(sum_out), _ptr(gram_out), int(f)))
+
+    def jump_distance(self, x, out, flags=0):
+        n, d = x.shape
+        _check(_lib.lgs_jump_distance(self._h, int(n), int(d), _ptr(x), int(d), _ptr(out),
+                                      int(flags | x_flags(x))))
+
+    def marginal_tvd(self, x1, x2, out, flags=0):
+        if _dtype_name(x1) != _dtype_name(x2):
+            raise TypeError("both sample sets must have the same dtype")
+        d = x1.shape[1]
+        _check(_lib.lgs_marginal_tvd(self._h, int(d), _ptr(x1), int(x1.shape[0]), _ptr(x2),
+                                     int(x2.shape[0]), _ptr(out), int(flags | x_flags(x1))))
 
     # ---------------------------------------------------------------- timing / info
     def timing_enable(self, on=True):

@@ -81,10 +81,15 @@ class DiscreteGaussianSampler(ABC):
         return self.stats
 
     def empirical_mean(self, samples: np.ndarray) -> np.ndarray:
-        return np.mean(samples, axis=0)
+        """np.mean(samples, axis=0) on the GPU (base.py:154-156)."""
+        from ..diagnostics import moments
+        return moments.empirical_mean(samples)
 
     def empirical_covariance(self, samples: np.ndarray) -> np.ndarray:
-        return np.cov(samples.T)
+        """np.cov(samples.T) on the GPU (base.py:158-160): exact int64 second moments
+        for integer-valued samples (lgs_gram, int8 MFMA)."""
+        from ..diagnostics import moments
+        return moments.empirical_covariance(samples)
 
     def theoretical_covariance(self) -> np.ndarray:
         return self.sigma ** 2 * np.eye(self.dimension)

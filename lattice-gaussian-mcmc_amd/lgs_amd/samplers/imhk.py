@@ -24,6 +24,7 @@ from typing import List, Optional, Tuple
 import numpy as np
 
 from .. import _capi
+from ..diagnostics import moments as _moments
 from .base import DiscreteGaussianSampler
 from .klein import RefinedKleinSampler, _default_seed
 
@@ -172,7 +173,7 @@ class IMHKSampler(DiscreteGaussianSampler):
             "acceptance_rate": self.stats.acceptance_rate,
             "spectral_gap_estimate": self.estimate_spectral_gap(100),
             "empirical_mean": self.empirical_mean(samples),
-            "empirical_std": np.std(samples, axis=0),
+            "empirical_std": _moments.empirical_std(samples),
             "theoretical_std": self.sigma * np.ones(self.dimension),
             "samples_per_second": num_samples / max(self.stats.time_elapsed, 1e-12),
         }

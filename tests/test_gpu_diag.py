@@ -1,0 +1,169 @@
+"""GPU: diagnostics kernels (csrc/lgs_diag.hip) through the C-ABI and the
+drop-in modules lgs_amd.diagnostics, against the reference-generated fixtures
+(tests/golden/diag_*.npz) and the oracle (oracle/lgs_diag_oracle.py).
+
+Tolerances: autocovariances are fp64 sums in a different (blocked) order than
+np.correlate / FFT -> relative 1e-10 on ACF values and derived scalars; integer
+moments, TVD and the window position of tau_int are exact.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_golden
+
+import lgs_diag_oracle as O
+
+pytestmark = pytest.mark.gpu
+SERIES = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "diag_series_*.npz")))
+RT = 1e-10
+
+
+@pytest.fixture(scope="module")
+def D():
+    from lgs_amd import diagnostics
+    return diagnostics
+
+
+@pytest.mark.parametrize("name", SERIES)
+def test_series_diagnostics_match_reference(D, name):
+    g = load_golden(name)
+    x = g["x"]
+    np.testing.assert_allclose(D.compute_autocorrelation(x), g["acf_direct"], rtol=RT, atol=1e-13)
+    np.testing.assert_allclose(D.mcmc_diag.compute_autocorrelation(x, 100), g["acf_direct_100"], rtol=RT,
+                               atol=1e-13)
+    np.testing.assert_allclose(D.convergence_diag.compute_autocorrelation(x), g["acf_fft"], rtol=RT,
+                               atol=1e-12)
+    np.testing.assert_allclose(D.integrated_autocorrelation_time(x), g["tau_direct"], rtol=RT)
+    np.testing.assert_allclose(D.convergence_diag.integrated_autocorrelation_time(x), g["tau_fft"], rtol=RT)
+    np.testing.assert_allclose(D.effective_sample_size(x), g["ess_autocorr"], rtol=RT)
+    np.testing.assert_allclose(D.effective_sample_size(x, "batch_means"), g["ess_batch"], rtol=RT)
+    np.testing.assert_allclose(D.compute_mcse(x, "batch"), g["mcse_batch"], rtol=RT)
+    np.testing.assert_allclose(D.compute_mcse(x, "spectral"), g["mcse_spectral"], rtol=RT)
+    np.testing.assert_allclose(D.batch_means_variance(x), g["bm_var"], rtol=RT)
+    dg = D.diagnose_chain(x)
+    for k in ("mean", "std", "ess", "ess_per_sample", "tau_int", "mean_jump_distance", "acf_lag_1",
+              "acf_lag_10"):
+        val = np.nan if dg[k] is None else dg[k]  # the fixture stores None as NaN
+        np.testing.assert_allclose(val, g["diag_" + k], rtol=RT, atol=1e-13, err_msg=k)
+    np.testing.assert_array_equal([dg["quantiles"][q] for q in ("2.5%", "25%", "50%", "75%", "97.5%")],
+                                  g["diag_quantiles"])
+
+
+def test_multivariate_trace_diagnostics(D):
+    g = load_golden("diag_trace_ntru32.npz")
+    z = g["z"]
+    for tag, x in (("z", z.astype(np.float64)), ("v", g["v"]), ("zh", z[:, 16:].astype(np.float64)),
+                   ("zh", np.ascontiguousarray(z[:, 16:]))):  # int64 input: exact sums
+        dg = D.diagnose_chain(x)
+        for k in ("ess", "ess_per_sample", "tau_int", "mean_jump_distance", "acf_lag_1", "acf_lag_10"):
+            np.testing.assert_allclose(dg[k], g[f"{tag}_{k}"], rtol=RT, atol=1e-13, err_msg=f"{tag} {k}")
+        np.testing.assert_array_equal(dg["mean"], g[f"{tag}_mean"])
+        np.testing.assert_allclose(dg["std"], g[f"{tag}_std"], rtol=1e-12)
+    np.testing.assert_allclose(D.effective_sample_size(z[:, 16:].astype(np.float64), "batch_means"),
+                               g["zh_ess_batch"], rtol=RT)
+    np.testing.assert_allclose(D.compute_jump_distance(z.astype(np.int32)), g["z_jumps"], rtol=1e-15)
+    np.testing.assert_allclose(D.empirical_covariance(g["v"]), g["v_cov"], rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(D.empirical_covariance(z), g["z_cov"], rtol=1e-12, atol=1e-9)
+
+
+def test_gelman_rubin_tvd_mixing(D):
+    g = load_golden("diag_gelman_rubin.npz")
+    chains = [g[f"chain{i}"] for i in range(5)]
+    np.testing.assert_allclose(D.gelman_rubin_statistic(chains), g["rhat"], rtol=RT)
+    t = load_golden("diag_tvd.npz")
+    assert D.compute_tvd(t["a"], t["b"]) == t["tvd"]                    # bit-identical
+    assert D.compute_tvd(t["a"][:, 4], t["b"][:, 4]) == t["tvd_1d"]
+    assert D.compute_tvd(t["a"].astype(np.int32), t["b"].astype(np.int32)) == t["tvd"]
+    assert D.mixing_time_estimate([0.9, 0.5, 0.3, 0.2, 0.1]) == t["mixing"]
+    with pytest.raises(Exception):
+        D.compute_tvd(t["a"] + 0.5, t["b"])                             # not integer-valued
+
+
+@pytest.mark.parametrize("n,d,lo,hi", [(1, 5, -3, 3), (63, 130, -32639, 32640), (1000, 128, -200, 200),
+                                       (4099, 257, -3000, 3000), (777, 33, -40000, 40000)])
+def test_gram_exact(D, n, d, lo, hi):
+    rng = np.random.default_rng(n * 7 + d)
+    z = rng.integers(lo, hi, size=(n, d)).astype(np.int32)
+    s_ref, G_ref = O.gram_exact(z)
+    s, G = D.gram(z)
+    np.testing.assert_array_equal(s, s_ref.astype(np.int64))
+    np.testing.assert_array_equal(G, G_ref.astype(np.int64))
+    s64, G64 = D.gram(z.astype(np.int64))
+    np.testing.assert_array_equal(G64, G)
+    sh = rng.integers(-50, 50, size=d)
+    s2, G2 = D.gram(z, shift=sh)
+    _, G2_ref = O.gram_exact(z.astype(np.int64) - sh)
+    np.testing.assert_array_equal(G2, G2_ref.astype(np.int64))
+
+
+def test_gram_accumulates_and_coordinate_major():
+    from lgs_amd import _capi
+    from lgs_amd.diagnostics import _gpu
+    ctx = _gpu.context()
+    rng = np.random.default_rng(5)
+    z = rng.integers(-900, 900, size=(300, 40)).astype(np.int32)
+    s = np.full(40, 7, dtype=np.int64)
+    G = np.ones((40, 40), dtype=np.int64)
+    ctx.gram(np.ascontiguousarray(z.T), sum_out=s, gram_out=G, coord_major=True)
+    _, G_ref = O.gram_exact(z)
+    np.testing.assert_array_equal(G, G_ref.astype(np.int64) + 1)
+    np.testing.assert_array_equal(s, z.sum(0) + 7)
+
+
+def test_covariance_real_and_device_tensors(D):
+    import torch
+    rng = np.random.default_rng(9)
+    x = rng.standard_normal((5000, 24)) * np.linspace(0.5, 3, 24) + 10.0
+    np.testing.assert_allclose(D.empirical_covariance(x), np.cov(x.T), rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(D.empirical_mean(x), np.mean(x, axis=0), rtol=1e-13)
+    xt = torch.as_tensor(x, device="cuda")
+    np.testing.assert_allclose(D.empirical_covariance(xt), np.cov(x.T), rtol=1e-10, atol=1e-12)
+    zi = np.round(x * 100).astype(np.int64)
+    zt = torch.as_tensor(zi, device="cuda")
+    np.testing.assert_allclose(D.empirical_covariance(zt), np.cov(zi.T.astype(np.float64)), rtol=1e-12)
+    np.testing.assert_allclose(D.effective_sample_size(xt), O.effective_sample_size(x), rtol=RT)
+    np.testing.assert_allclose(D.compute_jump_distance(xt), O.jump_distance(x), rtol=1e-14)
+    a = rng.integers(0, 2, size=1000).astype(bool)
+    assert D.compute_acceptance_rate(a) == np.mean(a)
+
+
+def test_series_long_and_strided_layouts():
+    """Chunked time axis (n > 4096), many lag blocks, IMHK-trace layout (chains x
+    steps x d) read in place, early-exit tau equals the full-scan tau."""
+    from lgs_amd.diagnostics import _gpu
+    rng = np.random.default_rng(11)
+    nc, T, d = 3, 9000, 5
+    e = rng.standard_normal((nc, T, d))
+    x = np.empty_like(e)
+    x[:, 0] = e[:, 0]
+    for t in range(1, T):
+        x[:, t] = 0.995 * x[:, t - 1] + 0.1 * e[:, t]
+    x = np.ascontiguousarray(x)
+    L = 700
+    r = _gpu.series_stats(x, n_series=nc * d, n=T, group_size=d, group_stride=T * d, series_stride=1,
+                          time_stride=d, max_lag=L, want=("mean", "c0", "acf", "tau"))
+    r2 = _gpu.series_stats(x, n_series=nc * d, n=T, group_size=d, group_stride=T * d, series_stride=1,
+                           time_stride=d, max_lag=L, want=("tau",))
+    for c in range(nc):
+        for i in range(d):
+            s = c * d + i
+            ref = O.autocorrelation_direct(x[c, :, i], L)
+            np.testing.assert_allclose(r["acf"][s], ref, rtol=1e-9, atol=1e-12)
+            np.testing.assert_allclose(r["tau"][s], O.tau_window(ref), rtol=1e-9)
+            assert r2["tau"][s] == r["tau"][s]
+            np.testing.assert_allclose(r["mean"][s], np.mean(x[c, :, i]), rtol=1e-12)
+
+
+def test_series_edge_cases(D):
+    # constant series: 0/0 -> NaN exactly like the reference (mcmc_diag.py:31)
+    acf = D.compute_autocorrelation(np.full(40, 3.0))
+    assert np.isnan(acf).all() and len(acf) == 11
+    assert np.isnan(D.integrated_autocorrelation_time(np.full(40, 3.0)))
+    # single sample
+    assert len(D.compute_autocorrelation(np.array([2.0]))) == 1
+    # max_lag beyond the series: numpy slicing keeps n lags
+    x = np.arange(6, dtype=np.float64)
+    np.testing.assert_allclose(D.compute_autocorrelation(x, 50), O.autocorrelation_direct(x, 50), rtol=1e-12)
