@@ -119,6 +119,9 @@ struct lgs_ctx {
     int64_t t_n[6] = {0, 0, 0, 0, 0, 0};
     // diagnostics scratch (lgs_series_stats / lgs_gram / lgs_jump_distance / lgs_marginal_tvd)
     DevBuf dg_x, dg_y, dg_out, dg_a, dg_b, dg_c;
+    // decoding frame (lgs_set_decoder): Q of the QR and (B^{-1})^T, row-major d x d
+    DevBuf DQ, DBIT;
+    bool has_q = false, has_binv = false;
     std::vector<Timer> pending;
     std::vector<hipEvent_t> pool;
 };
@@ -1320,6 +1323,128 @@ int lgs_marginal_tvd(lgs_ctx* c, int64_t d, const void* x1, int64_t n1, const vo
     HIP_TRY(lgs::launch::tvd_sum(c1, c2, off, (int)d, n1, n2, O, c->stream));
     if (!dev) HIP_TRY(hipMemcpyAsync(tvd_out, O, (size_t)d * 8, hipMemcpyDeviceToHost, c->stream));
     return finish(c);
+}
+
+}  // extern "C"
+
+// ============================================================ decoding
+namespace {
+
+// Shared driver of lgs_nearest_plane / lgs_round_decode: per chunk of targets,
+// W = M t on fp64 MFMA (M = Q^T or B^{-1}), then the nearest-plane walk or the
+// rounding, then z / v outputs as lgs_klein writes them.
+int run_decode(lgs_ctx* c, bool plane, int64_t n, const double* targets, void* z_out, double* v_out,
+               uint32_t flags) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    if (n < 0) return fail(LGS_ERR_INVALID, "n < 0");
+    if (n == 0) return LGS_OK;
+    if (!targets) return fail(LGS_ERR_INVALID, "null targets");
+    if (plane ? !c->has_q : !c->has_binv)
+        return fail(LGS_ERR_STATE, plane ? "nearest plane needs Q (lgs_set_decoder)"
+                                         : "rounding decode needs B^-1 (lgs_set_decoder)");
+    if (v_out && !c->has_B) return fail(LGS_ERR_STATE, "v_out requires B");
+    const bool dev = flags & LGS_DEVICE_PTRS, z64 = flags & LGS_Z64, cm = flags & LGS_COORD_MAJOR;
+    const int64_t d = c->d;
+    const int ob = z64 ? 8 : 4;
+    if ((rc = reset_flags(c))) return rc;
+    const int64_t chunk = std::min<int64_t>(n, std::max<int64_t>(256, ((int64_t)1 << 27) / d));
+    if ((rc = c->dg_x.reserve((size_t)chunk * d * 8)) || (rc = c->dg_y.reserve((size_t)chunk * d * 8)) ||
+        (rc = c->Z.reserve((size_t)chunk * d * ob)))
+        return rc;
+    if (!dev) {
+        if ((rc = c->stage_a.reserve((size_t)chunk * d * std::max(ob, 8)))) return rc;
+        if (v_out && (rc = c->V.reserve((size_t)chunk * d * 8))) return rc;
+    }
+    double* X = c->dg_x.as<double>();   // targets, coordinate-major (d x m)
+    double* Y = c->dg_y.as<double>();   // M t, row-major (m x d), then coordinate-major in X
+    for (int64_t off = 0; off < n; off += chunk) {
+        const int64_t m = std::min<int64_t>(chunk, n - off);
+        // targets -> X (d x m)
+        if (cm) {
+            for (int64_t i = 0; i < d; ++i)
+                HIP_TRY(hipMemcpyAsync(X + (size_t)i * m, targets + (size_t)i * n + off, (size_t)m * 8,
+                                       kind_of(true, dev), c->stream));
+        } else {
+            const double* src = targets + (size_t)off * d;
+            if (!dev) {
+                HIP_TRY(hipMemcpyAsync(c->stage_a.p, src, (size_t)m * d * 8, hipMemcpyHostToDevice, c->stream));
+                src = c->stage_a.as<double>();
+            }
+            HIP_TRY(lgs::launch::to_coord_major(src, 8, m, (int)d, X, 8, m, c->stream));
+        }
+        HIP_TRY(lgs::launch::gemm_f64(X, m, plane ? c->DQ.as<double>() : c->DBIT.as<double>(), (int)d, m, Y,
+                                      c->stream));
+        HIP_TRY(lgs::launch::to_coord_major(Y, 8, m, (int)d, X, 8, m, c->stream));
+        void* Zp = c->Z.p;
+        if (plane) {
+            const double* co = c->coord.as<double>();
+            HIP_TRY(lgs::launch::nearest_plane((int)d, m, c->panel, c->RP.as<double>(), c->RC.as<double>(),
+                                               co + d, X, m, ob, Zp, m, c->flags.as<unsigned int>(),
+                                               c->stream));
+        } else {
+            HIP_TRY(lgs::launch::round_coeffs(X, m, (int)d, m, ob, Zp, m, c->flags.as<unsigned int>(),
+                                              c->stream));
+        }
+        if (z_out) {
+            if (cm) {
+                for (int64_t i = 0; i < d; ++i)
+                    HIP_TRY(hipMemcpyAsync((char*)z_out + ((size_t)i * n + off) * ob, (char*)Zp + (size_t)i * m * ob,
+                                           (size_t)m * ob, kind_of(dev, true), c->stream));
+            } else {
+                void* dst = dev ? (char*)z_out + (size_t)off * d * ob : c->stage_a.p;
+                HIP_TRY(lgs::launch::transpose_out(Zp, ob, m, m, (int)d, dst, ob, c->stream));
+                if (!dev)
+                    HIP_TRY(hipMemcpyAsync((char*)z_out + (size_t)off * d * ob, dst, (size_t)m * d * ob,
+                                           hipMemcpyDeviceToHost, c->stream));
+            }
+        }
+        if (v_out) {
+            double* V = dev ? v_out + (size_t)off * d : c->V.as<double>();
+            if ((rc = run_bz(c, Zp, ob, m, m, V))) return rc;
+            if ((rc = settle_bz(c))) return rc;
+            if (!dev)
+                HIP_TRY(hipMemcpyAsync(v_out + (size_t)off * d, V, (size_t)m * d * 8, hipMemcpyDeviceToHost,
+                                       c->stream));
+        }
+        if ((rc = finish(c))) return rc;
+    }
+    return finish(c);
+}
+
+}  // namespace
+
+extern "C" {
+
+int lgs_set_decoder(lgs_ctx* c, const double* Q, const double* Binv) {
+    int rc = check_ctx(c);
+    if (rc) return rc;
+    const int64_t d = c->d;
+    const size_t bytes = (size_t)d * d * 8;
+    if (Q) {
+        if ((rc = c->DQ.reserve(bytes))) return rc;
+        HIP_TRY(hipMemcpy(c->DQ.p, Q, bytes, hipMemcpyHostToDevice));  // gemm_f64 reads Q[c][r]
+        c->has_q = true;
+    }
+    if (Binv) {
+        std::vector<double> t((size_t)d * d);
+        for (int64_t r = 0; r < d; ++r)
+            for (int64_t k = 0; k < d; ++k) t[(size_t)k * d + r] = Binv[(size_t)r * d + k];
+        if ((rc = c->DBIT.reserve(bytes))) return rc;
+        HIP_TRY(hipMemcpy(c->DBIT.p, t.data(), bytes, hipMemcpyHostToDevice));
+        c->has_binv = true;
+    }
+    return LGS_OK;
+}
+
+int lgs_nearest_plane(lgs_ctx* c, int64_t n, const double* targets, void* z_out, double* v_out,
+                      uint32_t flags) {
+    return run_decode(c, true, n, targets, z_out, v_out, flags);
+}
+
+int lgs_round_decode(lgs_ctx* c, int64_t n, const double* targets, void* z_out, double* v_out,
+                     uint32_t flags) {
+    return run_decode(c, false, n, targets, z_out, v_out, flags);
 }
 
 }  // extern "C"

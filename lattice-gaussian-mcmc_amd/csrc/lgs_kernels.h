@@ -180,6 +180,15 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, hipStream_t st);
+// ---- decoding
+// V (row-major n x d) = rows s: sum_c MT[c][r] X[c][s], X coordinate-major fp64 (fp64 MFMA)
+hipError_t gemm_f64(const double* X, int64_t ldx, const double* MT, int d, int64_t n, double* V,
+                    hipStream_t st);
+hipError_t nearest_plane(int d, int64_t n, int panel, const double* RP, const double* RC,
+                         const double* rii, const double* CP, int64_t ldc, int zb, void* Z, int64_t ldz,
+                         unsigned int* flags, hipStream_t st);
+hipError_t round_coeffs(const double* W, int64_t ldw, int d, int64_t n, int zb, void* Z, int64_t ldz,
+                        unsigned int* flags, hipStream_t st);
 hipError_t carry_cols(const void* zs, int ob, int zs_coord_major, int64_t nc, int d, void* Z, int zb,
                       int64_t ldz, int64_t col0, hipStream_t st);
 }  // namespace launch

@@ -262,6 +262,89 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
     if (flags) atomicOr(a.flags, flags);
 }
 
+// ------------------------------------------------------------ Babai nearest plane
+// Deterministic twin of klein_panel_kernel: the same panel
+// walk over R, with a per-target c' = Q^T t (coordinate-major CP[i][p]) and
+// z_i = round-half-even((c'_i - sum_{j>i} R_ij z_j) / R_ii) -- the nearest-plane
+// rule of src/lattices/base.py:105-135 in the QR frame (proj = <t, b*_i> /
+// <b*_i, b*_i> with t updated by the decided coefficients), i.e. Klein's mean
+// without the draw (klein.py:201-204).
+template <typename ZT, int PB>
+__global__ __launch_bounds__(256) void nearest_plane_kernel(int d, int64_t n,
+                                                            const double* __restrict__ RP,
+                                                            const double* __restrict__ RC,
+                                                            const double* __restrict__ rii,
+                                                            const double* __restrict__ CP, int64_t ldc,
+                                                            ZT* __restrict__ Z, int64_t ldz_,
+                                                            unsigned int* gflags) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const size_t ldz = (size_t)ldz_;
+    unsigned int flags = 0;
+    const int npan = (d + PB - 1) / PB;
+    double acc[PB];
+    for (int pk = 0; pk < npan; ++pk) {
+        const int p_hi = d - pk * PB;
+        const int rows = p_hi < PB ? p_hi : PB;
+#pragma unroll
+        for (int r = 0; r < PB; ++r) acc[r] = 0.0;
+        const double* __restrict__ rp = RP + (size_t)PB * PB * ((size_t)pk * (pk - 1) / 2);
+        int j = p_hi;
+        for (; j + 1 < d; j += 2) {
+            const double x0 = (double)Z[(size_t)j * ldz + p];
+            const double x1 = (double)Z[(size_t)(j + 1) * ldz + p];
+            const double* __restrict__ rj = rp + (size_t)(j - p_hi) * PB;
+#pragma unroll
+            for (int r = 0; r < PB; ++r) acc[r] = fma(rj[r], x0, acc[r]);
+#pragma unroll
+            for (int r = 0; r < PB; ++r) acc[r] = fma(rj[PB + r], x1, acc[r]);
+        }
+        if (j < d) {
+            const double x0 = (double)Z[(size_t)j * ldz + p];
+            const double* __restrict__ rj = rp + (size_t)(j - p_hi) * PB;
+#pragma unroll
+            for (int r = 0; r < PB; ++r) acc[r] = fma(rj[r], x0, acc[r]);
+        }
+        for (int s = 0; s < rows; ++s) {
+            const int i = p_hi - 1 - s;
+            const double mu = (CP[(size_t)i * ldc + p] - acc[PB - 1]) / cst(rii)[i];
+            double zi = 0.0;
+            if (isfinite(mu))
+                zi = rint(mu);
+            else
+                flags |= kFlagNonFinite;
+            store_z(Z, (size_t)i * ldz + p, zi, flags);
+            const cdptr rc = cst(RC) + (size_t)i * (PB - 1);
+#pragma unroll
+            for (int k = 0; k < PB - 1; ++k) acc[k] = fma(rc[PB - 2 - k], zi, acc[k]);
+#pragma unroll
+            for (int k = PB - 1; k >= 1; --k) acc[k] = acc[k - 1];
+            acc[0] = 0.0;
+        }
+    }
+    if (flags) atomicOr(gflags, flags);
+}
+
+// Babai rounding (src/lattices/simple.py:112-128, src/samplers/utils.py:575-577):
+// z = round-half-even(w), w = B^{-1} t given coordinate-major.
+template <typename ZT>
+__global__ __launch_bounds__(256) void round_kernel(const double* __restrict__ W, int64_t ldw, int d,
+                                                    int64_t n, ZT* __restrict__ Z, int64_t ldz,
+                                                    unsigned int* gflags) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = blockIdx.y;
+    if (p >= n) return;
+    unsigned int flags = 0;
+    const double w = W[(size_t)i * ldw + p];
+    double zi = 0.0;
+    if (isfinite(w))
+        zi = rint(w);
+    else
+        flags |= kFlagNonFinite;
+    store_z(Z, (size_t)i * ldz + p, zi, flags);
+    if (flags) atomicOr(gflags, flags);
+}
+
 // ------------------------------------------------------------ panel, MFMA far field
 // Same sampler and panel layout as klein_panel_kernel (PB = 16 or 32 rows), but
 // the far-field product of a panel -- F[PB rows][64 chains] = R_panel[PB x K] *
@@ -1401,6 +1484,35 @@ hipError_t bz(const void* Z, int zb, int64_t ldz, const int64_t* sel, const doub
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
     LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_gemm_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, BT, d, n, V, ldv, rb, rstride, roff));
+    return hipGetLastError();
+}
+
+hipError_t gemm_f64(const double* X, int64_t ldx, const double* MT, int d, int64_t n, double* V,
+                    hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
+    hipLaunchKernelGGL(bz_gemm_kernel<double>, grid, dim3(256), 0, st, X, ldx, nullptr, MT, d, n, V,
+                       (int64_t)d, n, (int64_t)0, (int64_t)0);
+    return hipGetLastError();
+}
+
+hipError_t nearest_plane(int d, int64_t n, int panel, const double* RP, const double* RC,
+                         const double* rii, const double* CP, int64_t ldc, int zb, void* Z, int64_t ldz,
+                         unsigned int* flags, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (panel == 16)
+        LGS_ZT(zb, ZT, hipLaunchKernelGGL((nearest_plane_kernel<ZT, 16>), grid, dim3(256), 0, st, d, n, RP, RC, rii, CP, ldc, (ZT*)Z, ldz, flags));
+    else
+        LGS_ZT(zb, ZT, hipLaunchKernelGGL((nearest_plane_kernel<ZT, 32>), grid, dim3(256), 0, st, d, n, RP, RC, rii, CP, ldc, (ZT*)Z, ldz, flags));
+    return hipGetLastError();
+}
+
+hipError_t round_coeffs(const double* W, int64_t ldw, int d, int64_t n, int zb, void* Z, int64_t ldz,
+                        unsigned int* flags, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + 255) / 256), (unsigned)d);
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(round_kernel<ZT>, grid, dim3(256), 0, st, W, ldw, d, n, (ZT*)Z, ldz, flags));
     return hipGetLastError();
 }
 

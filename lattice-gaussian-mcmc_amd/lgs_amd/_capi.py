@@ -42,7 +42,8 @@ KERNEL_GRAM, KERNEL_SERIES = 4, 5
 EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_destroy", "lgs_set_stream",
            "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_lattice_points", "lgs_log_density", "lgs_sample_z", "lgs_timing_enable",
            "lgs_timing_get", "lgs_device_info", "lgs_series_stats", "lgs_gram",
-           "lgs_jump_distance", "lgs_marginal_tvd")
+           "lgs_jump_distance", "lgs_marginal_tvd", "lgs_set_decoder", "lgs_nearest_plane",
+           "lgs_round_decode")
 
 
 class LgsError(RuntimeError):
@@ -101,6 +102,9 @@ def load_library(path: str = LIB_PATH):
     L.lgs_gram.argtypes = [_vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp, ctypes.c_uint32]
     L.lgs_jump_distance.argtypes = [_vp, _i64, _i64, _vp, _i64, _vp, ctypes.c_uint32]
     L.lgs_marginal_tvd.argtypes = [_vp, _i64, _vp, _i64, _vp, _i64, _vp, ctypes.c_uint32]
+    L.lgs_set_decoder.argtypes = [_vp, _vp, _vp]
+    L.lgs_nearest_plane.argtypes = [_vp, _i64, _vp, _vp, _vp, ctypes.c_uint32]
+    L.lgs_round_decode.argtypes = [_vp, _i64, _vp, _vp, _vp, ctypes.c_uint32]
     for name in EXPORTS:
         if name not in ("lgs_version", "lgs_last_error"):
             getattr(L, name).restype = ctypes.c_int
@@ -247,6 +251,38 @@ class Context:
         _check(_lib.lgs_sample_z(self._h, mu.size, _ptr(mu), _ptr(sg), _ptr(uu), int(precision),
                                  _ptr(z), _ptr(ln), f))
         return z, ln
+
+    # ---------------------------------------------------------------- decoding
+    def set_decoder(self, Q=None, Binv=None):
+        Qc = None if Q is None else np.ascontiguousarray(Q, dtype=np.float64)
+        Bi = None if Binv is None else np.ascontiguousarray(Binv, dtype=np.float64)
+        for M in (Qc, Bi):
+            if M is not None and M.shape != (self.d, self.d):
+                raise ValueError("decoder matrices must be d x d")
+        _check(_lib.lgs_set_decoder(self._h, _ptr(Qc), _ptr(Bi)))
+        self._keep_dec = (Qc, Bi)
+
+    def decode(self, targets, method="plane", z_out=None, v_out=None, flags=0):
+        """Raw lgs_nearest_plane / lgs_round_decode on caller buffers."""
+        fn = _lib.lgs_nearest_plane if method == "plane" else _lib.lgs_round_decode
+        n = targets.shape[1] if flags & LGS_COORD_MAJOR else targets.shape[0]
+        _check(fn(self._h, int(n), _ptr(targets), _ptr(z_out), _ptr(v_out), int(flags)))
+
+    def decode_host(self, targets, method="plane", want_v=True):
+        """Decode host targets (n x d); int32 coefficients first, int64 on overflow."""
+        t = np.ascontiguousarray(targets, dtype=np.float64)
+        n = t.shape[0]
+        for z64 in (False, True):
+            z = np.empty((n, self.d), dtype=np.int64 if z64 else np.int32)
+            v = np.empty((n, self.d)) if want_v else None
+            try:
+                self.decode(t, method, z, v, LGS_Z64 if z64 else 0)
+            except LgsError as e:
+                if e.code == LGS_ERR_OVERFLOW and not z64:
+                    continue
+                raise
+            return z.astype(np.int64, copy=False), v
+        raise AssertionError("unreachable")
 
     # ---------------------------------------------------------------- diagnostics
     def series_stats(self, x, n_series, n, group_size, group_stride, series_stride, time_stride,
