@@ -1,0 +1,110 @@
+"""GPU: full-size statistical and size-independent properties of the sampler
+(north_star: "empirical covariance / IMHK acceptance match within 1%").
+
+* Z^64, sigma = 5 (config C1 shape, 2^16 samples): the empirical covariance of
+  the GPU samples (exact int64 second moments, lgs_gram) is within 1% of the
+  exact discrete-Gaussian variance on the diagonal, and the first samples are
+  bit-exact against the oracle.
+* NTRU n=512 (d = 1024, config C3 basis), Wang-Ling IMHK on 2^14 chains: the
+  accept decisions of a chain subset are bit-exact against the CPU oracle on
+  the same counters, and the acceptance over all chains agrees with the oracle's
+  subset estimate within its binomial error; reference-mode acceptance is 1.0
+  exactly, as the reference's.
+* Checksum of checksums: the IMHK moment accumulators (moments_kernel) equal the
+  sums of the kept states recomputed by an independent reduction (lgs_gram).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _dgauss_var(sigma):
+    k = np.arange(-60 * int(np.ceil(sigma)), 60 * int(np.ceil(sigma)) + 1, dtype=np.float64)
+    w = np.exp(-k * k / (2 * sigma * sigma))
+    return float((k * k * w).sum() / w.sum())
+
+
+def test_z64_empirical_covariance_within_1pct(oracle):
+    from lgs_amd import _capi, diagnostics
+    from lgs_amd.lattices import identity_basis
+    import torch
+    d, sigma, n = 64, 5.0, 1 << 16
+    B = identity_basis(d)
+    R, cp = oracle.qr_prepare(B)
+    ctx = _capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    z = torch.empty((n, d), dtype=torch.int32, device="cuda")
+    ctx.klein(4242, 0, n, z, None, None, _capi.LGS_DEVICE_PTRS)
+    s, G = diagnostics.gram(z)
+    cov = (G.astype(np.float64) - np.outer(s, s) / n) / (n - 1)
+    var = _dgauss_var(sigma)
+    diag = np.diag(cov)
+    assert abs(diag.mean() / var - 1) < 0.01
+    assert np.all(np.abs(diag / var - 1) < 0.03)                      # 5.4 sigma per coordinate
+    off = cov[~np.eye(d, dtype=bool)]
+    assert np.all(np.abs(off) < 6 * var / np.sqrt(n))
+    assert np.all(np.abs(s / n) < 6 * np.sqrt(var / n))
+    o = oracle.klein(R, cp, sigma, 512, seed=4242)
+    assert np.array_equal(z[:512].cpu().numpy(), o["z"])
+    np.testing.assert_allclose(diagnostics.empirical_covariance(z[:512].cpu().numpy()),
+                               np.cov(o["z"].T.astype(np.float64)), rtol=1e-12, atol=1e-12)
+
+
+def test_ntru1024_imhk_acceptance_full_size(oracle):
+    from lgs_amd import _capi
+    from lgs_amd.lattices import build_config
+    import torch
+    lat, sigma = build_config("C3_ntru512")
+    B = lat.basis
+    d = B.shape[0]
+    R, cp = oracle.qr_prepare(B)
+    ctx = _capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    nc, T, seed = 1 << 14, 4, 99
+    out = {}
+    for wl in (False, True):
+        z = torch.zeros((d, nc), dtype=torch.int32, device="cuda")
+        lw = torch.zeros(nc, dtype=torch.float64, device="cuda")
+        init = torch.zeros(nc, dtype=torch.int32, device="cuda")
+        acc = torch.zeros(nc, dtype=torch.int64, device="cuda")
+        f = _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR | (_capi.LGS_WANG_LING if wl else 0)
+        ctx.imhk(seed, 0, nc, 1, T, 1, z, lw, init, acc, flags=f)
+        out[wl] = (acc.cpu().numpy(), z[:, :16].cpu().numpy().T)
+    assert out[False][0].sum() == nc * T                                # reference weight: always accept
+    acc_wl, z_wl = out[True]
+    m = 16
+    zo, _, acco = oracle.imhk_parallel(R, cp, B, sigma, m, T, seed=seed, first_step=1,
+                                       mode=oracle.IMHK_WANG_LING, threads=8)
+    assert np.array_equal(acc_wl[:m], acco)                              # bit-exact decisions
+    assert np.array_equal(z_wl[:m], zo)
+    rate, rate_sub = acc_wl.mean() / T, acco.mean() / T
+    se = np.sqrt(max(rate_sub * (1 - rate_sub), 1e-4) / (m * T))
+    assert abs(rate - rate_sub) < 4 * se + 1e-12
+
+
+def test_moments_checksum_of_checksums():
+    from lgs_amd import _capi, diagnostics
+    from lgs_amd.lattices import build_config
+    import lgs_oracle
+    import torch
+    lat, sigma = build_config("C2_qary128")
+    B = lat.basis
+    d = B.shape[0]
+    R, cp = lgs_oracle.qr_prepare(B)
+    ctx = _capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    nc, T = 4096, 8
+    z = torch.zeros((nc, d), dtype=torch.int32, device="cuda")
+    lw = torch.zeros(nc, dtype=torch.float64, device="cuda")
+    init = torch.zeros(nc, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(nc, dtype=torch.int64, device="cuda")
+    zs = torch.zeros((nc, T, d), dtype=torch.int32, device="cuda")
+    mom = torch.zeros(2 * d, dtype=torch.int64, device="cuda")
+    ctx.imhk(5, 0, nc, 1, T, 1, z, lw, init, acc, z_samples=zs, moments=mom,
+             flags=_capi.LGS_DEVICE_PTRS | _capi.LGS_WANG_LING)
+    flat = zs.reshape(-1, d)
+    s, G = diagnostics.gram(flat)
+    m = mom.cpu().numpy()
+    assert np.array_equal(m[:d], s)
+    assert np.array_equal(m[d:], np.diag(G))
