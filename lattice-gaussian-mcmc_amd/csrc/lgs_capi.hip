@@ -118,7 +118,7 @@ struct lgs_ctx {
     double t_ms[6] = {0, 0, 0, 0, 0, 0};
     int64_t t_n[6] = {0, 0, 0, 0, 0, 0};
     // diagnostics scratch (lgs_series_stats / lgs_gram / lgs_jump_distance / lgs_marginal_tvd)
-    DevBuf dg_x, dg_y, dg_out, dg_a, dg_b, dg_c;
+    DevBuf dg_x, dg_y, dg_out, dg_a, dg_b, dg_c, dg_t;
     // decoding frame (lgs_set_decoder): Q of the QR and (B^{-1})^T, row-major d x d
     DevBuf DQ, DBIT;
     bool has_q = false, has_binv = false;
@@ -655,8 +655,9 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     c->sigma = sigma;
     c->precision = precision;
     c->basis_flags = flags;
-    // proposals per launch: keep the coefficient store around <= 2 GiB
-    const int64_t cap = std::max<int64_t>(256, (int64_t)((size_t)2 << 30) / (8 * d));
+    // proposals per launch: keep the coefficient store around <= 8 GiB (288 GB of HBM;
+    // d = 4096 still gets 2^18 lanes = 4096 waves, enough to fill the 256 CUs)
+    const int64_t cap = std::max<int64_t>(256, (int64_t)((size_t)8 << 30) / (8 * d));
     if (!getenv("LGS_MAX_PROPOSALS")) c->max_props = std::min<int64_t>(std::max<int64_t>(cap, 256), 1 << 20);
     return LGS_OK;
 }
@@ -1184,14 +1185,6 @@ int lgs_gram(lgs_ctx* c, int64_t d, int64_t n, const void* x, int64_t ldx, const
     const size_t xbytes = cm ? ((size_t)(d - 1) * ldx + n) * xb : (size_t)n * d * xb;
     const void* Xin = nullptr;
     if ((rc = dev_in(c, dev, x, xbytes, c->dg_x, Xin))) return rc;
-    const void* Xc = Xin;
-    int64_t ld = ldx;
-    if (!cm) {  // row-major -> coordinate-major scratch (8-byte elements move as bit patterns)
-        if ((rc = c->dg_y.reserve((size_t)n * d * xb))) return rc;
-        HIP_TRY(lgs::launch::to_coord_major(Xin, xb, n, (int)d, c->dg_y.p, xb, n, c->stream));
-        Xc = c->dg_y.p;
-        ld = n;
-    }
     const void* SH = nullptr;
     if (shift && (rc = dev_in(c, dev, shift, (size_t)d * 8, c->dg_c, SH))) return rc;
     // accumulators: the caller's (device) or staged copies of the host values (ADDED to)
@@ -1215,28 +1208,39 @@ int lgs_gram(lgs_ctx* c, int64_t d, int64_t n, const void* x, int64_t ldx, const
                 HIP_TRY(hipMemsetAsync(S, 0, sbytes, c->stream));
         }
     }
-    const bool i8 = xt != 0;
-    if (i8) {  // keep the accumulators' prior values for an exact replay
-        if ((rc = c->dg_out.reserve(gbytes + sbytes))) return rc;
-        HIP_TRY(hipMemcpyAsync(c->dg_out.p, G, gbytes, hipMemcpyDeviceToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync((char*)c->dg_out.p + gbytes, S, sbytes, hipMemcpyDeviceToDevice, c->stream));
-    }
-    {
-        Scope s(c, 4);
-        HIP_TRY(lgs::launch::gram(Xc, xt, ld, (int)d, n, i8, SH, G, S, c->flags.as<unsigned int>(),
-                                  c->stream));
-    }
-    if (i8) {
+    bool valu = xt == 0;
+    if (!valu) {  // int8 digit planes, then the MFMA Gram (exact while |x - shift| <= 32639)
+        const int64_t ldp = (n + 63) / 64 * 64, dpad = (d + 127) / 128 * 128;
+        if ((rc = c->dg_y.reserve((size_t)2 * dpad * ldp))) return rc;
+        int8_t* Ph = c->dg_y.as<int8_t>();
+        int8_t* Pl = Ph + (size_t)dpad * ldp;
         unsigned int f = 0;
+        {
+            Scope s(c, 4);
+            HIP_TRY(lgs::launch::gram_pack(Xin, xt, cm, ldx, (int)d, n, (const long long*)SH, Ph, Pl, ldp,
+                                           c->flags.as<unsigned int>(), c->stream));
+        }
         HIP_TRY(hipMemcpyAsync(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
-        if (f & lgs::kFlagI8Range) {  // some |x - shift| > 32639: exact int64 VALU replay
-            HIP_TRY(hipMemcpyAsync(G, c->dg_out.p, gbytes, hipMemcpyDeviceToDevice, c->stream));
-            HIP_TRY(hipMemcpyAsync(S, (char*)c->dg_out.p + gbytes, sbytes, hipMemcpyDeviceToDevice, c->stream));
+        if (f & lgs::kFlagI8Range) {
+            valu = true;  // some |x - shift| > 32639: exact int64 VALU
+            HIP_TRY(hipMemsetAsync(c->flags.p, 0, 16, c->stream));
+        } else {
             Scope s(c, 4);
-            HIP_TRY(lgs::launch::gram(Xc, xt, ld, (int)d, n, false, SH, G, S, nullptr, c->stream));
+            HIP_TRY(lgs::launch::gram_planes(Ph, Pl, ldp, (int)d, G, S, c->stream));
         }
-        HIP_TRY(hipMemsetAsync(c->flags.p, 0, 16, c->stream));
+    }
+    if (valu) {
+        const void* Xc = Xin;
+        int64_t ld = ldx;
+        if (!cm) {  // row-major -> coordinate-major (8-byte elements move as bit patterns)
+            if ((rc = c->dg_t.reserve((size_t)n * d * xb))) return rc;
+            HIP_TRY(lgs::launch::to_coord_major(Xin, xb, n, (int)d, c->dg_t.p, xb, n, c->stream));
+            Xc = c->dg_t.p;
+            ld = n;
+        }
+        Scope s(c, 4);
+        HIP_TRY(lgs::launch::gram(Xc, xt, ld, (int)d, n, SH, G, S, c->stream));
     }
     if (!dev) {
         if (gram_out) HIP_TRY(hipMemcpyAsync(gram_out, G, gbytes, hipMemcpyDeviceToHost, c->stream));

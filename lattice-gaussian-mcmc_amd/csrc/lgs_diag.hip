@@ -6,7 +6,7 @@
 //                        (mcmc_diag.py:36-56, convergence_diag.py:116-145) with an
 //                        early exit once the window closes, and batch means
 //                        (mcmc_diag.py:79-98, 228-241; convergence_diag.py:316-345).
-//   gram_i8_kernel       exact integer second moments  sum_s z z^T  and  sum_s z of
+//   gram_planes_kernel   exact integer second moments  sum_s z z^T  and  sum_s z of
 //                        coefficient vectors (empirical mean / covariance,
 //                        base.py:154-160) on v_mfma_i32_32x32x32_i8 with two balanced
 //                        base-256 digits per coefficient; gram_val_kernel is the exact
@@ -177,41 +177,6 @@ __global__ __launch_bounds__(256) void series_stats_kernel(SeriesArgs a) {
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v16i_t __attribute__((ext_vector_type(16)));
 
-template <typename ZT>
-__device__ __forceinline__ void gram_stage(const ZT* __restrict__ Z, int64_t ldz, int d, int64_t k,
-                                           int64_t k1, int r0, int tid, int8_t* D1, int8_t* D0,
-                                           const long long* __restrict__ shift, bool& bad,
-                                           long long* zsum) {
-    constexpr int P = 80;
-    const int row = tid >> 2, part = tid & 3;
-    const int gr = r0 + row;
-    const int64_t kk = k + part * 16;
-    const ZT* zp = Z + (size_t)gr * ldz + kk;
-    const bool rok = gr < d;
-    const long long sh = (rok && shift) ? shift[gr] : 0;
-    v4i_t w0, w1;
-#pragma unroll
-    for (int qd = 0; qd < 4; ++qd) {
-        unsigned int lo4 = 0, hi4 = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int e = qd * 4 + j;
-            const long long zr = (rok && kk + e < k1) ? (long long)zp[e] - sh : 0;
-            bad |= (zr > 32639) | (zr < -32639);
-            const int z = (int)zr;
-            if (zsum) *zsum += zr;
-            const int lo = (z << 24) >> 24;
-            const int hi = (z - lo) >> 8;
-            lo4 |= ((unsigned int)lo & 0xffu) << (8 * j);
-            hi4 |= ((unsigned int)hi & 0xffu) << (8 * j);
-        }
-        w0[qd] = (int)lo4;
-        w1[qd] = (int)hi4;
-    }
-    *(v4i_t*)&D0[row * P + part * 16] = w0;
-    *(v4i_t*)&D1[row * P + part * 16] = w1;
-}
-
 __device__ __forceinline__ void atomic_add_val(long long* p, long long v) {
     atomicAdd((unsigned long long*)p, (unsigned long long)v);
 }
@@ -227,13 +192,82 @@ __device__ __forceinline__ void tile_pair(int p, int nt, int& ti, int& tj) {
     tj = i + p;
 }
 
-template <typename ZT>
-__global__ __launch_bounds__(512) void gram_i8_kernel(const ZT* __restrict__ Z, int64_t ldz, int d,
-                                                      int64_t n, int64_t kc, int nt,
-                                                      const long long* __restrict__ shift,
-                                                      unsigned long long* __restrict__ G,
-                                                      unsigned long long* __restrict__ S,
-                                                      unsigned int* flags) {
+// (1) gram_pack_kernel: y = x - shift -> balanced base-256 digit planes
+//     Ph / Pl [coordinate][sample] int8 (row pitch ldp = n rounded up to 64, rows
+//     up to d rounded up to 128, padding zero), read once from row-major (n x d)
+//     or coordinate-major (d x n) input through a 64 x 64 LDS tile.
+// (2) gram_planes_kernel: block tile 128 x 128 of the upper block triangle, 8 waves
+//     as 2 x 4 (64 x 32 each = two 32x32 MFMA tiles), K steps of 64 samples: the
+//     next step's 16-byte plane pieces are loaded into registers right after the
+//     barrier, so the loads overlap the 16 MFMAs per wave of the current step.
+//     K chunks of kc <= 16384 samples per workgroup keep the int32 class sums exact
+//     (2 kc 2^14 < 2^31); results are ADDED with 64-bit atomics.
+// (3) gram_mirror_kernel copies the upper block triangle into the lower one.
+template <typename ZT, bool CM>
+__global__ __launch_bounds__(256) void gram_pack_kernel(const ZT* __restrict__ X, int64_t ldx, int d,
+                                                        int64_t n, const long long* __restrict__ shift,
+                                                        int8_t* __restrict__ Ph, int8_t* __restrict__ Pl,
+                                                        int64_t ldp, unsigned int* flags) {
+    __shared__ int tile[64][65];  // [coordinate][sample]
+    const int tid = threadIdx.x;
+    const int64_t s0 = (int64_t)blockIdx.x * 64;
+    const int c0 = blockIdx.y * 64;
+    bool bad = false;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        // coalesced along the contiguous axis of the input
+        const int fast = tid & 63, slow = e * 4 + (tid >> 6);
+        const int cc = CM ? slow : fast, ss = CM ? fast : slow;
+        const int c = c0 + cc;
+        const int64_t s = s0 + ss;
+        long long y = 0;
+        if (c < d && s < n) {
+            y = CM ? (long long)X[(size_t)c * ldx + s] : (long long)X[(size_t)s * ldx + c];
+            if (shift) y -= shift[c];
+            bad |= (y > 32639) | (y < -32639);
+        }
+        tile[cc][ss] = (int)y;
+    }
+    __syncthreads();
+    const int cc = tid >> 2, part = tid & 3;
+    v4i_t wl, wh;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        unsigned int lo4 = 0, hi4 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int y = tile[cc][part * 16 + q * 4 + j];
+            const int lo = (y << 24) >> 24;
+            const int hi = (y - lo) >> 8;
+            lo4 |= ((unsigned int)lo & 0xffu) << (8 * j);
+            hi4 |= ((unsigned int)hi & 0xffu) << (8 * j);
+        }
+        wl[q] = (int)lo4;
+        wh[q] = (int)hi4;
+    }
+    const size_t off = (size_t)(c0 + cc) * ldp + s0 + part * 16;
+    *(v4i_t*)(Pl + off) = wl;
+    *(v4i_t*)(Ph + off) = wh;
+    if (bad) atomicOr(flags, kFlagI8Range);
+}
+
+__device__ __forceinline__ int digit_sum16(v4i_t h, v4i_t l) {  // sum of 256 h + l over 16 bytes
+    int s = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int hb = (h[q] << (24 - 8 * j)) >> 24, lb = (l[q] << (24 - 8 * j)) >> 24;
+            s += 256 * hb + lb;
+        }
+    return s;
+}
+
+__global__ __launch_bounds__(512) void gram_planes_kernel(const int8_t* __restrict__ Ph,
+                                                          const int8_t* __restrict__ Pl, int64_t ldp,
+                                                          int d, int64_t np, int64_t kc, int nt,
+                                                          unsigned long long* __restrict__ G,
+                                                          unsigned long long* __restrict__ S) {
     constexpr int BT = 128, KC = 64, P = 80;
     __shared__ __attribute__((aligned(16))) int8_t A1[BT * P], A0[BT * P], B1[BT * P], B0[BT * P];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -242,7 +276,12 @@ __global__ __launch_bounds__(512) void gram_i8_kernel(const ZT* __restrict__ Z, 
     tile_pair((int)blockIdx.x, nt, ti, tj);
     const bool diag = ti == tj;
     const int64_t k0 = (int64_t)blockIdx.y * kc;
-    const int64_t k1 = k0 + kc < n ? k0 + kc : n;
+    const int64_t k1 = k0 + kc < np ? k0 + kc : np;
+    const int row = tid >> 2, part = tid & 3;
+    const int8_t* pa_h = Ph + (size_t)(ti * BT + row) * ldp + part * 16;
+    const int8_t* pa_l = Pl + (size_t)(ti * BT + row) * ldp + part * 16;
+    const int8_t* pb_h = Ph + (size_t)(tj * BT + row) * ldp + part * 16;
+    const int8_t* pb_l = Pl + (size_t)(tj * BT + row) * ldp + part * 16;
     v16i_t h[2], m[2], l[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -250,14 +289,33 @@ __global__ __launch_bounds__(512) void gram_i8_kernel(const ZT* __restrict__ Z, 
         m[t] = (v16i_t){};
         l[t] = (v16i_t){};
     }
-    bool bad = false;
-    long long zsum = 0;
+    int zsum = 0;
+    v4i_t rah = *(const v4i_t*)(pa_h + k0), ral = *(const v4i_t*)(pa_l + k0);
+    v4i_t rbh = rah, rbl = ral;
+    if (!diag) {
+        rbh = *(const v4i_t*)(pb_h + k0);
+        rbl = *(const v4i_t*)(pb_l + k0);
+    }
     const int8_t* Bh = diag ? A1 : B1;
     const int8_t* Bl = diag ? A0 : B0;
     for (int64_t k = k0; k < k1; k += KC) {
-        gram_stage<ZT>(Z, ldz, d, k, k1, ti * BT, tid, A1, A0, shift, bad, diag ? &zsum : nullptr);
-        if (!diag) gram_stage<ZT>(Z, ldz, d, k, k1, tj * BT, tid, B1, B0, shift, bad, nullptr);
+        *(v4i_t*)&A1[row * P + part * 16] = rah;
+        *(v4i_t*)&A0[row * P + part * 16] = ral;
+        if (!diag) {
+            *(v4i_t*)&B1[row * P + part * 16] = rbh;
+            *(v4i_t*)&B0[row * P + part * 16] = rbl;
+        } else {
+            zsum += digit_sum16(rah, ral);
+        }
         __syncthreads();
+        if (k + KC < k1) {  // next step's pieces in flight during the MFMAs
+            rah = *(const v4i_t*)(pa_h + k + KC);
+            ral = *(const v4i_t*)(pa_l + k + KC);
+            if (!diag) {
+                rbh = *(const v4i_t*)(pb_h + k + KC);
+                rbl = *(const v4i_t*)(pb_l + k + KC);
+            }
+        }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int kb = ks * 32 + 16 * (lane >> 5);
@@ -285,14 +343,23 @@ __global__ __launch_bounds__(512) void gram_i8_kernel(const ZT* __restrict__ Z, 
             const int gj = tj * BT + wn * 32 + (lane & 31);
             if (gi < d && gj < d) {
                 const long long v = 65536LL * h[rt][reg] + 256LL * m[rt][reg] + (long long)l[rt][reg];
-                if (v) {
-                    atomicAdd(G + (size_t)gi * d + gj, (unsigned long long)v);
-                    if (!diag) atomicAdd(G + (size_t)gj * d + gi, (unsigned long long)v);
-                }
+                if (v) atomicAdd(G + (size_t)gi * d + gj, (unsigned long long)v);
             }
         }
-    if (diag && S && zsum) atomicAdd(S + ti * BT + (tid >> 2), (unsigned long long)zsum);
-    if (bad) atomicOr(flags, kFlagI8Range);
+    if (diag && S) {  // 4 threads per row: reduce across the part lanes, one atomic per row
+        zsum += __shfl_xor(zsum, 1, 64);
+        zsum += __shfl_xor(zsum, 2, 64);
+        const int gi = ti * BT + row;
+        if (part == 0 && gi < d && zsum) atomicAdd(S + gi, (unsigned long long)(long long)zsum);
+    }
+}
+
+// lower block triangle := upper (tiles ti < tj of 128); diagonal tiles are full
+__global__ __launch_bounds__(256) void gram_mirror_kernel(unsigned long long* __restrict__ G, int d) {
+    const int j = blockIdx.x * 16 + (threadIdx.x & 15);   // column of the lower entry
+    const int i = blockIdx.y * 16 + (threadIdx.x >> 4);   // row
+    if (i >= d || j >= d || (i >> 7) <= (j >> 7)) return;
+    G[(size_t)i * d + j] = G[(size_t)j * d + i];
 }
 
 // VALU Gram: exact int64 replay for integer data (any |z - shift| < 2^31 with sums
@@ -475,31 +542,56 @@ int64_t gram_chunk(int64_t n, int nt) {
     return kc;
 }
 
-hipError_t gram(const void* Z, int xtype, int64_t ldz, int d, int64_t n, bool i8, const void* shift,
-                void* G, void* S, unsigned int* flags, hipStream_t st) {
+hipError_t gram(const void* Z, int xtype, int64_t ldz, int d, int64_t n, const void* shift, void* G,
+                void* S, hipStream_t st) {
     if (n <= 0 || d <= 0) return hipSuccess;
-    if (i8 && xtype != 0) {
-        const int nt = (d + 127) / 128;
-        const int64_t kc = gram_chunk(n, nt);
-        const dim3 grid((unsigned)(nt * (nt + 1) / 2), (unsigned)((n + kc - 1) / kc));
-        auto g = (unsigned long long*)G;
-        auto sm = (unsigned long long*)S;
-        auto sh = (const long long*)shift;
-        if (xtype == 2)
-            hipLaunchKernelGGL(gram_i8_kernel<int64_t>, grid, dim3(512), 0, st, (const int64_t*)Z, ldz, d, n, kc, nt, sh, g, sm, flags);
+    const int nt = (d + 63) / 64;
+    const int64_t kc = gram_chunk(n, nt);
+    const dim3 grid((unsigned)(nt * (nt + 1) / 2), (unsigned)((n + kc - 1) / kc));
+    if (xtype == 2)
+        hipLaunchKernelGGL((gram_val_kernel<int64_t, long long>), grid, dim3(256), 0, st, (const int64_t*)Z, ldz, d, n, kc, nt, (const long long*)shift, (long long*)G, (long long*)S);
+    else if (xtype == 1)
+        hipLaunchKernelGGL((gram_val_kernel<int32_t, long long>), grid, dim3(256), 0, st, (const int32_t*)Z, ldz, d, n, kc, nt, (const long long*)shift, (long long*)G, (long long*)S);
+    else
+        hipLaunchKernelGGL((gram_val_kernel<double, double>), grid, dim3(256), 0, st, (const double*)Z, ldz, d, n, kc, nt, (const double*)shift, (double*)G, (double*)S);
+    return hipGetLastError();
+}
+
+hipError_t gram_pack(const void* X, int xtype, bool coord_major, int64_t ldx, int d, int64_t n,
+                     const long long* shift, int8_t* Ph, int8_t* Pl, int64_t ldp, unsigned int* flags,
+                     hipStream_t st) {
+    const int dpad = (d + 127) / 128 * 128;
+    const dim3 grid((unsigned)(ldp / 64), (unsigned)(dpad / 64));
+    if (xtype == 2) {
+        if (coord_major)
+            hipLaunchKernelGGL((gram_pack_kernel<int64_t, true>), grid, dim3(256), 0, st, (const int64_t*)X, ldx, d, n, shift, Ph, Pl, ldp, flags);
         else
-            hipLaunchKernelGGL(gram_i8_kernel<int32_t>, grid, dim3(512), 0, st, (const int32_t*)Z, ldz, d, n, kc, nt, sh, g, sm, flags);
+            hipLaunchKernelGGL((gram_pack_kernel<int64_t, false>), grid, dim3(256), 0, st, (const int64_t*)X, ldx, d, n, shift, Ph, Pl, ldp, flags);
     } else {
-        const int nt = (d + 63) / 64;
-        const int64_t kc = gram_chunk(n, nt);
-        const dim3 grid((unsigned)(nt * (nt + 1) / 2), (unsigned)((n + kc - 1) / kc));
-        if (xtype == 2)
-            hipLaunchKernelGGL((gram_val_kernel<int64_t, long long>), grid, dim3(256), 0, st, (const int64_t*)Z, ldz, d, n, kc, nt, (const long long*)shift, (long long*)G, (long long*)S);
-        else if (xtype == 1)
-            hipLaunchKernelGGL((gram_val_kernel<int32_t, long long>), grid, dim3(256), 0, st, (const int32_t*)Z, ldz, d, n, kc, nt, (const long long*)shift, (long long*)G, (long long*)S);
+        if (coord_major)
+            hipLaunchKernelGGL((gram_pack_kernel<int32_t, true>), grid, dim3(256), 0, st, (const int32_t*)X, ldx, d, n, shift, Ph, Pl, ldp, flags);
         else
-            hipLaunchKernelGGL((gram_val_kernel<double, double>), grid, dim3(256), 0, st, (const double*)Z, ldz, d, n, kc, nt, (const double*)shift, (double*)G, (double*)S);
+            hipLaunchKernelGGL((gram_pack_kernel<int32_t, false>), grid, dim3(256), 0, st, (const int32_t*)X, ldx, d, n, shift, Ph, Pl, ldp, flags);
     }
+    return hipGetLastError();
+}
+
+hipError_t gram_planes(const int8_t* Ph, const int8_t* Pl, int64_t ldp, int d, void* G, void* S,
+                       hipStream_t st) {
+    const int nt = (d + 127) / 128;
+    const int64_t pairs = (int64_t)nt * (nt + 1) / 2;
+    // about 2 workgroups (16 waves) per CU, K chunks of 64..16384 samples
+    int64_t splits = (512 + pairs - 1) / pairs;
+    int64_t kc = (ldp + splits - 1) / splits;
+    kc = (kc + 63) / 64 * 64;
+    if (kc > 16384) kc = 16384;
+    if (kc < 64) kc = 64;
+    const dim3 grid((unsigned)pairs, (unsigned)((ldp + kc - 1) / kc));
+    hipLaunchKernelGGL(gram_planes_kernel, grid, dim3(512), 0, st, Ph, Pl, ldp, d, ldp, kc, nt,
+                       (unsigned long long*)G, (unsigned long long*)S);
+    if (nt > 1)
+        hipLaunchKernelGGL(gram_mirror_kernel, dim3((unsigned)((d + 15) / 16), (unsigned)((d + 15) / 16)),
+                           dim3(256), 0, st, (unsigned long long*)G, d);
     return hipGetLastError();
 }
 

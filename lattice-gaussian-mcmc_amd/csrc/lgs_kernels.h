@@ -136,12 +136,19 @@ namespace launch {
 // ---- diagnostics (lgs_diag.hip); xtype 0 fp64, 1 int32, 2 int64
 hipError_t series_stats(const SeriesArgs& a, hipStream_t st);
 // sum y y^T (d x d, both triangles) and sum y (d), y = x - shift (shift nullable),
-// ADDED to G / S: int64 for integer x (xtype 1 int32, 2 int64; shift int64), fp64
-// for xtype 0 (shift fp64).  x coordinate-major (d x n, ld ldz).
-// i8 (integer x): int8-digit MFMA path, sets kFlagI8Range when |y| > 32639 (redo
-// with i8 = false: exact int64 VALU)
-hipError_t gram(const void* Z, int xtype, int64_t ldz, int d, int64_t n, bool i8, const void* shift,
-                void* G, void* S, unsigned int* flags, hipStream_t st);
+// ADDED to G / S; x coordinate-major (d x n, ld ldz).  VALU: exact int64 for
+// integer x (xtype 1 int32, 2 int64; shift int64), fp64 for xtype 0 (shift fp64).
+hipError_t gram(const void* Z, int xtype, int64_t ldz, int d, int64_t n, const void* shift, void* G,
+                void* S, hipStream_t st);
+// int8-digit path: pack y = x - shift into digit planes Ph / Pl ((d rounded up to
+// 128) rows x ldp bytes, ldp = n rounded up to 64; sets kFlagI8Range when some
+// |y| > 32639), then the MFMA Gram of the planes (upper block triangle + mirror:
+// G must be symmetric on entry).
+hipError_t gram_pack(const void* X, int xtype, bool coord_major, int64_t ldx, int d, int64_t n,
+                     const long long* shift, int8_t* Ph, int8_t* Pl, int64_t ldp, unsigned int* flags,
+                     hipStream_t st);
+hipError_t gram_planes(const int8_t* Ph, const int8_t* Pl, int64_t ldp, int d, void* G, void* S,
+                       hipStream_t st);
 hipError_t jump(const void* x, int xtype, int64_t n, int d, int64_t ld, double* out, hipStream_t st);
 hipError_t tvd_minmax(const void* x, int xtype, int64_t n, int d, long long* mn, long long* mx,
                       unsigned int* flags, hipStream_t st);
