@@ -164,6 +164,48 @@ class IMHKSampler(DiscreteGaussianSampler):
         mx = float(np.max(w))
         return 1.0 / mx if mx > 0 else 0.0
 
+    # ------------------------------------------------------------ Wang-Ling delta
+    def _log_normaliser_max(self) -> float:
+        """log prod_i rho_{sigma_i}(Z) over the drawn coordinates (sigma_i >= 1e-10):
+        each 1-D normaliser is largest at an integer mean (Poisson summation), so this
+        is the maximum of the Wang-Ling weight.  Evaluated by the device SampleZ
+        normaliser (lgs_sample_z) at mu = 0 with the sampler's window rules."""
+        if getattr(self, "_lnmax", None) is None:
+            R = self.proposal_sampler.R
+            sig = self.sigma / np.abs(np.diag(R))
+            sig = sig[sig >= 1e-10]
+            sig = np.where(sig > 1e10, 1e6, sig)
+            _, ln = self.context.sample_z(np.zeros(sig.size), sig, np.full(sig.size, 0.5),
+                                          precision=self.proposal_sampler.precision)
+            self._lnmax = float(np.sum(ln))
+        return self._lnmax
+
+    def compute_delta(self, num_samples: int = 1 << 16) -> float:
+        """Monte Carlo estimate of Wang & Ling's delta = rho_{sigma,c}(L) / prod_i rho_{sigma_i}(Z)
+        (the quantity of imhk.py:256-258 and the aspirational IndependentMHK.compute_delta of
+        experiments/cryptographic_experiments.py:288): rho(L) = E_Klein[w(x)] with the exact
+        weight w(x) = prod_i rho_{sigma_i}(Z - mu_i(x)), drawn on the GPU
+        (lgs_klein with LGS_WANG_LING log-weights)."""
+        r = self.proposal_sampler._draw(int(num_samples), want_v=False, want_logw=True,
+                                        flags=_capi.LGS_WANG_LING)
+        lw = r["logw"]
+        m = float(np.max(lw))
+        log_mean = m + float(np.log(np.mean(np.exp(lw - m))))
+        return float(np.exp(log_mean - self._log_normaliser_max()))
+
+    def spectral_gap(self, num_samples: int = 1 << 16) -> float:
+        """Spectral gap of the IMHK kernel: delta (uniform ergodicity, ||P^t - pi|| <= (1-delta)^t)."""
+        return self.compute_delta(num_samples)
+
+    def mixing_time(self, epsilon: float = 0.25, num_samples: int = 1 << 16) -> int:
+        """t_mix(epsilon) <= ceil(ln(epsilon) / ln(1 - delta))."""
+        delta = self.compute_delta(num_samples)
+        if delta >= 1.0:
+            return 1
+        if delta <= 0.0:
+            return int(np.iinfo(np.int64).max)
+        return int(np.ceil(np.log(epsilon) / np.log1p(-delta)))
+
     def diagnose_convergence(self, num_samples: int = 1000) -> dict:
         """imhk.py:286-313."""
         old_stats = self.stats

@@ -108,3 +108,31 @@ def test_moments_checksum_of_checksums():
     m = mom.cpu().numpy()
     assert np.array_equal(m[:d], s)
     assert np.array_equal(m[d:], np.diag(G))
+
+
+def test_wang_ling_delta_matches_enumeration():
+    """compute_delta (no reference implementation -- parity unpinned,
+    checked against the exact delta of small lattices by enumeration)."""
+    from lgs_amd.lattices import SimpleLattice
+    from lgs_amd.samplers import IMHKSampler
+    B = np.array([[4.0, 1.0], [1.0, 3.0]])
+    sigma = 2.0
+    s = IMHKSampler(SimpleLattice(B), sigma, burn_in=0, seed=17)
+    Q, R = np.linalg.qr(B)
+    sig_i = sigma / np.abs(np.diag(R))
+    k = np.arange(-200, 201)
+    log_norm_max = sum(np.log(np.exp(-k * k / (2 * si * si)).sum()) for si in sig_i)
+    g = np.arange(-60, 61)
+    Z = np.stack(np.meshgrid(g, g), -1).reshape(-1, 2).astype(np.float64)
+    V = Z @ B.T
+    rho_L = np.exp(-(V * V).sum(1) / (2 * sigma * sigma)).sum()
+    delta_true = rho_L / np.exp(log_norm_max)
+    n = 1 << 18
+    delta = s.compute_delta(n)
+    assert 0 < delta <= 1
+    assert abs(delta / delta_true - 1) < 0.01
+    t = s.mixing_time(0.25, n)
+    assert abs(t - int(np.ceil(np.log(0.25) / np.log1p(-delta)))) <= 1   # fresh draws: delta moves slightly
+    # identity lattice, zero center: the weight is constant, delta = 1
+    sI = IMHKSampler(SimpleLattice(np.eye(6)), 1.5, burn_in=0, seed=3)
+    assert abs(sI.compute_delta(4096) - 1.0) < 1e-12
