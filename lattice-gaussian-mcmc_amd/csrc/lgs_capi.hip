@@ -955,10 +955,16 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
             Scope s(c, 2);
             HIP_TRY(lgs::launch::accept(aa, c->stream));
         }
+        // The final-state gather rides on the moments pass unless a later step of this
+        // block still reads the carried-in states (kept-state gather without carry columns).
+        const bool fuse_final = moments && !(z_samples && kb > 0 && !carry) && npb < ((int64_t)1 << 32);
         if (moments) {
             Scope s(c, 3);
-            HIP_TRY(lgs::launch::moments(c->Z.p, zb, ldzb, c->cnt.as<int32_t>(), npb, (int)d, mom, c->stream));
+            // carried-in states first: the fused pass overwrites z_state
             HIP_TRY(lgs::launch::moments_carry(zs, ob, cm, nc, (int)d, c->ccnt.as<int32_t>(), mom, c->stream));
+            HIP_TRY(lgs::launch::moments_final(c->Z.p, zb, ldzb, c->cnt.as<int32_t>(), npb, Tb,
+                                               fuse_final ? c->fsel.as<int64_t>() : nullptr, (int)d, mom, zs,
+                                               ob, cm, nc, c->stream));
         }
         if ((z_samples || v_samples) && kb > 0) {
             // kept states q = chain*kb + k, gathered coordinate-major (d x nq); chain-major
@@ -983,8 +989,9 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
             }
         }
         // chain states after the block (in place; carried chains keep their row)
-        HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, ldzb, c->fsel.as<int64_t>(), nc, 1, zs, ob, cm, nc,
-                                      (int)d, zs, cm, c->stream));
+        if (!fuse_final)
+            HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, ldzb, c->fsel.as<int64_t>(), nc, 1, zs, ob, cm, nc,
+                                          (int)d, zs, cm, c->stream));
         if ((rc = finish(c))) return rc;
     }
     if (!dev) {

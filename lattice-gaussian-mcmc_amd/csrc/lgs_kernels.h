@@ -168,6 +168,10 @@ hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, int z
                        hipStream_t st);
 hipError_t moments(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int d,
                    unsigned long long* mom, hipStream_t st);
+// moments of the proposal store + (fsel non-null) the chains' final states into zs
+hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int64_t T,
+                         const int64_t* fsel, int d, unsigned long long* mom, void* zs, int ob,
+                         int zs_cm, int64_t nc, hipStream_t st);
 hipError_t moments_carry(const void* zs, int zb, int coord_major, int64_t nc, int d,
                          const int32_t* cc, unsigned long long* mom, hipStream_t st);
 hipError_t gather_z(const void* Z, int zb, int64_t ldz, const int64_t* sel, int64_t nq,

@@ -1007,6 +1007,69 @@ __global__ __launch_bounds__(256) void moments_kernel(const ZT* __restrict__ Z, 
     }
 }
 
+// Moments of the retained states and the chains' final states in one pass over
+// the proposal store: mom[i] += sum_p cnt[p] z[i][p], mom[d+i] += sum_p cnt[p]
+// z[i][p]^2, and where final_sel[p / T] == p (fsel non-null) the value is also the
+// chain's new state, written to z_state in the caller's layout -- the final-state
+// gather folded into the pass that already reads every proposal (a separate
+// gather touches one proposal in T per cache line).  VEC: four consecutive
+// proposals per lane in one 8/16/32-byte load (ldz % 4 == 0, n % 4 == 0).
+template <typename ZT, typename OT, bool VEC>
+__global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict__ Z, int64_t ldz,
+                                                            const int32_t* __restrict__ cnt, int64_t n,
+                                                            int64_t T, const int64_t* __restrict__ fsel,
+                                                            int d, int64_t chunk,
+                                                            unsigned long long* mom,
+                                                            OT* __restrict__ zs, int zs_cm, int64_t nc) {
+    const int i = blockIdx.y;
+    const int64_t p0 = (int64_t)blockIdx.x * chunk;
+    const int64_t p1 = p0 + chunk < n ? p0 + chunk : n;
+    const ZT* __restrict__ zr = Z + (size_t)i * ldz;
+    long long s1 = 0, s2 = 0;
+    auto one = [&](int64_t p, long long z, long long w) {
+        s1 += w * z;
+        s2 += w * z * z;
+        if (fsel) {
+            const int64_t c = (int64_t)((uint32_t)p / (uint32_t)T);  // n < 2^32 (checked by the caller)
+            if (fsel[c] == p) {
+                if (zs_cm)
+                    zs[(size_t)i * nc + c] = (OT)z;
+                else
+                    zs[(size_t)c * d + i] = (OT)z;
+            }
+        }
+    };
+    if constexpr (VEC) {
+        typedef ZT zv4_t __attribute__((ext_vector_type(4)));
+        typedef int iv4_t __attribute__((ext_vector_type(4)));
+        for (int64_t p = p0 + 4 * (int64_t)threadIdx.x; p < p1; p += 1024) {
+            const zv4_t zv = *(const zv4_t*)(zr + p);
+            const iv4_t wv = cnt ? *(const iv4_t*)(cnt + p) : (iv4_t){1, 1, 1, 1};
+            one(p, (long long)zv[0], wv[0]);
+            one(p + 1, (long long)zv[1], wv[1]);
+            one(p + 2, (long long)zv[2], wv[2]);
+            one(p + 3, (long long)zv[3], wv[3]);
+        }
+    } else {
+        for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) one(p, (long long)zr[p], cnt ? cnt[p] : 1);
+    }
+    __shared__ long long r1[256], r2[256];
+    r1[threadIdx.x] = s1;
+    r2[threadIdx.x] = s2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            r1[threadIdx.x] += r1[threadIdx.x + o];
+            r2[threadIdx.x] += r2[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd(mom + i, (unsigned long long)r1[0]);
+        atomicAdd(mom + d + i, (unsigned long long)r2[0]);
+    }
+}
+
 // Carried-in states (row-major or coordinate-major z_state) weighted by cnt_carry.
 template <typename ZT>
 __global__ __launch_bounds__(256) void moments_carry_kernel(const ZT* __restrict__ zs,
@@ -1427,6 +1490,23 @@ hipError_t moments(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64
     const int64_t chunk = 16384;
     const dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
     LGS_ZT(zb, ZT, hipLaunchKernelGGL(moments_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, d, chunk, mom));
+    return hipGetLastError();
+}
+
+hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int64_t T,
+                         const int64_t* fsel, int d, unsigned long long* mom, void* zs, int ob,
+                         int zs_cm, int64_t nc, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t chunk = 16384;  // multiple of 4
+    const dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
+    const bool vec = ldz % 4 == 0 && n % 4 == 0 && ((uintptr_t)Z % (4 * (uintptr_t)zb)) == 0 &&
+                     (!cnt || ((uintptr_t)cnt % 16) == 0);
+    LGS_ZT(zb, ZT, LGS_ZT(ob, OT, {
+        if (vec)
+            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, true>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc);
+        else
+            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, false>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc);
+    }));
     return hipGetLastError();
 }
 

@@ -517,3 +517,38 @@ def test_imhk_device_v_samples(ctx, capi):
     assert np.array_equal(vs.cpu().numpy(), np.einsum("rc,nkc->nkr", B, zsn))
     assert np.array_equal(z.cpu().numpy().T, zr.cpu().numpy())
     assert torch.equal(acc, acc2)
+
+
+@pytest.mark.parametrize("nc,steps,cm", [(64, 12, True), (37, 7, True), (40, 9, False)])
+def test_imhk_fused_final_state_with_moments(ctx, capi, oracle, nc, steps, cm):
+    """Moments + lattice points (carry columns) take the fused moments/final-state
+    pass (vectorised when the store is 4-aligned, scalar otherwise); Wang-Ling
+    weights make chains reject, so some chains keep their carried-in state.
+    Final states, moments and acceptances equal the oracle's."""
+    import torch
+    g = load_golden("klein_ntru32.npz")
+    R, cp, B = golden_R(g)
+    sigma = float(g["sigma"])
+    ctx.set_basis(R, cp, B, sigma)
+    d = R.shape[0]
+    dev = "cuda:0"
+    z = torch.zeros((d, nc) if cm else (nc, d), dtype=torch.int32, device=dev)
+    lw = torch.zeros(nc, dtype=torch.float64, device=dev)
+    init = torch.zeros(nc, dtype=torch.int32, device=dev)
+    acc = torch.zeros(nc, dtype=torch.int64, device=dev)
+    mom = torch.zeros(2 * d, dtype=torch.int64, device=dev)
+    vs = torch.zeros((nc, steps, d), dtype=torch.float64, device=dev)
+    f = capi.LGS_DEVICE_PTRS | capi.LGS_WANG_LING | (capi.LGS_COORD_MAJOR if cm else 0)
+    half = steps // 2
+    ctx.imhk(31, 0, nc, 1, half, 1, z, lw, init, acc, v_samples=vs[:, :half].contiguous(), moments=mom, flags=f)
+    ctx.imhk(31, 0, nc, 1 + half, steps - half, 1, z, lw, init, acc,
+             v_samples=vs[:, half:].contiguous(), moments=mom, flags=f)
+    o = oracle.imhk(R, cp, B, sigma, nc, steps, seed=31, first_step=1, mode=oracle.IMHK_WANG_LING, trace=True)
+    zf = z.cpu().numpy()
+    assert np.array_equal(zf.T if cm else zf, o["z"])
+    assert np.array_equal(acc.cpu().numpy(), o["accepts"])
+    assert 0 < o["accepts"].sum() < nc * steps
+    flat = o["trace"].reshape(-1, d).astype(np.int64)
+    m = mom.cpu().numpy()
+    assert np.array_equal(m[:d], flat.sum(0))
+    assert np.array_equal(m[d:], (flat * flat).sum(0))
