@@ -1026,18 +1026,11 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
     const int64_t p1 = p0 + chunk < n ? p0 + chunk : n;
     const ZT* __restrict__ zr = Z + (size_t)i * ldz;
     long long s1 = 0, s2 = 0;
-    auto one = [&](int64_t p, long long z, long long w) {
-        s1 += w * z;
-        s2 += w * z * z;
-        if (fsel) {
-            const int64_t c = (int64_t)((uint32_t)p / (uint32_t)T);  // n < 2^32 (checked by the caller)
-            if (fsel[c] == p) {
-                if (zs_cm)
-                    zs[(size_t)i * nc + c] = (OT)z;
-                else
-                    zs[(size_t)c * d + i] = (OT)z;
-            }
-        }
+    auto put = [&](int64_t c, long long z) {
+        if (zs_cm)
+            zs[(size_t)i * nc + c] = (OT)z;
+        else
+            zs[(size_t)c * d + i] = (OT)z;
     };
     if constexpr (VEC) {
         typedef ZT zv4_t __attribute__((ext_vector_type(4)));
@@ -1045,13 +1038,26 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
         for (int64_t p = p0 + 4 * (int64_t)threadIdx.x; p < p1; p += 1024) {
             const zv4_t zv = *(const zv4_t*)(zr + p);
             const iv4_t wv = cnt ? *(const iv4_t*)(cnt + p) : (iv4_t){1, 1, 1, 1};
-            one(p, (long long)zv[0], wv[0]);
-            one(p + 1, (long long)zv[1], wv[1]);
-            one(p + 2, (long long)zv[2], wv[2]);
-            one(p + 3, (long long)zv[3], wv[3]);
+            const long long z0 = zv[0], z1 = zv[1], z2 = zv[2], z3 = zv[3];
+            s1 += wv[0] * z0 + wv[1] * z1 + wv[2] * z2 + wv[3] * z3;
+            s2 += wv[0] * z0 * z0 + wv[1] * z1 * z1 + wv[2] * z2 * z2 + wv[3] * z3 * z3;
+            if (fsel) {  // chains whose proposals touch [p, p+3] (one, two at a boundary)
+                for (uint32_t c = (uint32_t)p / (uint32_t)T; (int64_t)c * T <= p + 3 && (int64_t)c < nc; ++c) {
+                    const int64_t k = fsel[c] - p;
+                    if (k >= 0 && k < 4) put(c, k == 0 ? z0 : k == 1 ? z1 : k == 2 ? z2 : z3);
+                }
+            }
         }
     } else {
-        for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) one(p, (long long)zr[p], cnt ? cnt[p] : 1);
+        for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+            const long long z = (long long)zr[p], w = cnt ? cnt[p] : 1;
+            s1 += w * z;
+            s2 += w * z * z;
+            if (fsel) {
+                const int64_t c = (int64_t)((uint32_t)p / (uint32_t)T);  // n < 2^32 (checked by the caller)
+                if (fsel[c] == p) put(c, z);
+            }
+        }
     }
     __shared__ long long r1[256], r2[256];
     r1[threadIdx.x] = s1;
