@@ -84,6 +84,13 @@ struct CoordStream {
         pair = 0xffffffffu;
     }
     __device__ __forceinline__ double u(uint32_t slot) {
+#ifdef LGS_DIAG_CHEAP_RNG  // diagnostic builds only: Philox cost probe (wrong stream)
+        uint32_t hh = (slot * 0x9E3779B9u) ^ (chain * 0x85EBCA6Bu) ^ step ^ k0;
+        hh ^= hh >> 15;
+        hh *= 0x2C1B3C6Du;
+        hh ^= hh >> 12;
+        return (double)hh * 0x1p-32;
+#endif
         const uint32_t p = slot >> 1;
         if (p != pair) {
             w = philox4x32_10(p, step, chain, kTagCoord, k0, k1);

@@ -410,6 +410,9 @@ struct ZQuad<int64_t> {
 // tile 0 is parked in the per-wave scratch f0 and moved into the LDS tile once
 // the upper rows are loaded (the LDS tile is free during the upper sub-panel).
 typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+#ifndef LGS_OZ_NG  // 16-sample groups per far-field pass (1 or 2)
+#define LGS_OZ_NG 2
+#endif
 
 __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_hi, int64_t p0, int lane,
                                              lds_cdptr rec, double* F, int LDF, double (&acc)[16],
@@ -452,27 +455,32 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
         for (int m = 0; m < 4; ++m)
             if (tid + 256 * m < SLAB) ash4[buf * SLAB + tid + 256 * m] = pf[m];
     };
-    // two passes of two 16-sample groups: each A fragment read from LDS feeds 4 MFMAs
+    // 4/NG passes of NG 16-sample groups: each A fragment read from LDS feeds 2 NG MFMAs
+    constexpr int NG = LGS_OZ_NG;
 #pragma unroll 1
-    for (int gp = 0; gp < 2; ++gp) {
-        v4i32_t cc[2][2][8];  // [group][row tile][class]
+    for (int gp = 0; gp < 4 / NG; ++gp) {
+        v4i32_t cc[NG][2][8];  // [group][row tile][class]
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < NG; ++q)
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int c = 0; c < 8; ++c) cc[q][t][c] = (v4i32_t){0, 0, 0, 0};
-        const int16_t* __restrict__ hb0 = a.h16 + (blk0 * a.h16_lanes + p0 + 32 * gp + n) * 16;
-        const int16_t* __restrict__ hb1 = hb0 + 16 * 16;  // group 2gp + 1: 16 lanes further
+        const int16_t* __restrict__ hb0 = a.h16 + (blk0 * a.h16_lanes + p0 + 16 * NG * gp + n) * 16;
+        const int16_t* __restrict__ hb1 = hb0 + 16 * 16;  // group NG gp + 1: 16 lanes further
         v4i32_t pf[4];
-        v4u_t w[2][2];
+        v4u_t w[NG][2];
         auto hist_load = [&](int ch) {
             const v4u_t* h0 = (const v4u_t*)(hb0 + (size_t)ch * hstep);
             const v4u_t* h1 = (const v4u_t*)(hb1 + (size_t)ch * hstep);
             w[0][0] = __builtin_nontemporal_load(h0);
             w[0][1] = __builtin_nontemporal_load(h0 + 1);
-            w[1][0] = __builtin_nontemporal_load(h1);
-            w[1][1] = __builtin_nontemporal_load(h1 + 1);
+            if constexpr (NG == 2) {
+                w[NG - 1][0] = __builtin_nontemporal_load(h1);
+                w[NG - 1][1] = __builtin_nontemporal_load(h1 + 1);
+            } else {
+                (void)h1;
+            }
         };
         __syncthreads();  // previous pass done with both buffers
         int cur = next_live(0);
@@ -486,9 +494,9 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
         __syncthreads();
 #pragma unroll 1
         for (int it = 0; cur < nch; ++it) {
-            v4i32_t xh[2], xl[2];  // history of chunk ch -> digit planes, per group
+            v4i32_t xh[NG], xl[NG];  // history of chunk ch -> digit planes, per group
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
+            for (int q = 0; q < NG; ++q) {
                 const v4u_t w0 = w[q][0], w1 = w[q][1];
                 xh[q][0] = (int)__builtin_amdgcn_perm(w0[1], w0[0], 0x07050301u);
                 xh[q][1] = (int)__builtin_amdgcn_perm(w0[3], w0[2], 0x07050301u);
@@ -513,7 +521,7 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
                     const v4i32_t av = sl[(t * kOzDigits + dg) * 64];
                     // digit a = dg + 1: class a - 1 with the high x digit, class a with the low
 #pragma unroll
-                    for (int q = 0; q < 2; ++q) {
+                    for (int q = 0; q < NG; ++q) {
                         cc[q][t][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xh[q], cc[q][t][dg], 0, 0, 0);
                         cc[q][t][dg + 1] =
                             __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xl[q], cc[q][t][dg + 1], 0, 0, 0);
@@ -525,12 +533,12 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
         }
         // classes -> fp64; D layout: rows 4h + reg of the tile, sample 16g + n
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < NG; ++q)
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int reg = 0; reg < 4; ++reg) {
-                    const int g = 2 * gp + q;
+                    const int g = NG * gp + q;
                     const int row = 16 * t + 4 * h + reg;  // panel row = record index
                     double sv = (double)cc[q][t][7][reg];
 #pragma unroll
@@ -559,6 +567,9 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
 #ifndef LGS_MFMA_LB32
 #define LGS_MFMA_LB32 3
 #endif
+#ifndef LGS_OZ_LB  // waves per SIMD the int8-digit far-field kernel is compiled for
+#define LGS_OZ_LB 2
+#endif
 // Diagnostic builds (-DLGS_DIAG_CYCLES): per-wave shader-clock accounting of the
 // 32-row-panel kernel, summed over waves into lgs_diag_cycles (lane 0 adds):
 // [0] record staging + barriers, [1] far field, [2] near field, [3 + kind] the
@@ -575,7 +586,7 @@ __device__ unsigned long long lgs_diag_cycles[16];
 // OZ (32-row panels only): far field as an exact int8-digit product on
 // v_mfma_i32_16x16x64_i8 instead of fp64 MFMA (see oz_far_field).
 template <typename ZT, int PB, bool WL, bool OZ = false>
-__global__ __launch_bounds__(256, PB == 32 ? (OZ ? 2 : LGS_MFMA_LB32) : 3) void klein_mfma_kernel(const KleinArgs a,
+__global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 3) void klein_mfma_kernel(const KleinArgs a,
                                                             const double* __restrict__ RP,
                                                             const double* __restrict__ RC,
                                                             ZT* __restrict__ Z) {
