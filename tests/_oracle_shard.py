@@ -7,15 +7,23 @@ from lgs_amd.distributed import ShardResult
 
 
 def oracle_compute_factory(oracle, R, cp, B, sigma, seed, *, thin: int = 1, mode: int = 0,
-                           center: Optional[np.ndarray] = None):
+                           center: Optional[np.ndarray] = None, want_gram: bool = False,
+                           gr_coord: Optional[int] = None):
     """CPU stand-in for `gpu_compute` (the oracle module is passed in by the test)."""
     d = R.shape[0]
 
     def compute(first_chain, n_chains, first_step, n_steps):
         st = oracle.imhk(R, cp, B, sigma, n_chains, n_steps, center=center, seed=seed,
                          first_chain=first_chain, first_step=first_step, mode=mode, trace=True)
-        kept = st["trace"][:, thin - 1::thin].reshape(-1, d)
+        tr = st["trace"][:, thin - 1::thin]
+        kept = tr.reshape(-1, d)
         mom = np.concatenate([kept.sum(0), (kept * kept).sum(0)]).astype(np.int64)
-        return ShardResult(int(st["accepts"].sum()), mom, kept.shape[0])
+        gram = kept.T.astype(np.int64) @ kept.astype(np.int64) if want_gram else None
+        cs = None
+        if gr_coord is not None:
+            x = tr[:, :, gr_coord].astype(np.float64)
+            m = x.mean(1)
+            cs = np.stack([m, ((x - m[:, None]) ** 2).sum(1)], 1)
+        return ShardResult(int(st["accepts"].sum()), mom, kept.shape[0], gram, cs)
 
     return compute

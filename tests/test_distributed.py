@@ -38,9 +38,10 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     g = load_golden("klein_ntru32.npz")
     R, cp, B = golden_R(g)
-    comp = oracle_compute_factory(lgs_oracle, R, cp, B, float(g["sigma"]), 4242, thin=2)
-    acc, mom, kept = imhk_sharded(comp, 7, 10, rank=rank, world=world)
-    out[rank] = (acc, mom.tolist(), kept)
+    comp = oracle_compute_factory(lgs_oracle, R, cp, B, float(g["sigma"]), 4242, thin=2,
+                                  mode=lgs_oracle.IMHK_WANG_LING, want_gram=True, gr_coord=31)
+    js = imhk_sharded(comp, 7, 10, rank=rank, world=world)
+    out[rank] = (js.accepts, js.moments.tolist(), js.kept, js.gram.tolist(), js.chain_stats.tolist())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -63,9 +64,21 @@ def test_gloo_world2_matches_single_process(oracle):
     mp.start_processes(_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
     g = load_golden("klein_ntru32.npz")
     R, cp, B = golden_R(g)
-    single = oracle_compute_factory(oracle, R, cp, B, float(g["sigma"]), 4242, thin=2)(0, 7, 1, 10)
+    single = oracle_compute_factory(oracle, R, cp, B, float(g["sigma"]), 4242, thin=2,
+                                    mode=oracle.IMHK_WANG_LING, want_gram=True, gr_coord=31)(0, 7, 1, 10)
+    from lgs_amd.distributed import JobStats
     for rank in (0, 1):
-        acc, mom, kept = out[rank]
+        acc, mom, kept, gram, cs = out[rank]
         assert acc == single.accepts
         assert kept == single.kept == 7 * 5
         assert np.array_equal(np.array(mom), single.moments)
+        assert np.array_equal(np.array(gram), single.gram)                 # all-reduced sum z z^T
+        np.testing.assert_array_equal(np.array(cs), single.chain_stats)    # gathered, global order
+        js = JobStats(acc, np.array(mom), kept, np.array(gram), np.array(cs))
+        flat = oracle.imhk(R, cp, B, float(g["sigma"]), 7, 10, seed=4242, first_step=1,
+                           mode=oracle.IMHK_WANG_LING, trace=True)["trace"][:, 1::2]
+        np.testing.assert_allclose(js.covariance(), np.cov(flat.reshape(-1, R.shape[0]).T.astype(float)),
+                                   rtol=1e-12, atol=1e-12)
+        import lgs_diag_oracle as O
+        np.testing.assert_allclose(js.gelman_rubin(5), O.gelman_rubin([c for c in flat[:, :, 31].astype(float)]),
+                                   rtol=1e-12)

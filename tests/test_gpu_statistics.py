@@ -136,3 +136,30 @@ def test_wang_ling_delta_matches_enumeration():
     # identity lattice, zero center: the weight is constant, delta = 1
     sI = IMHKSampler(SimpleLattice(np.eye(6)), 1.5, burn_in=0, seed=3)
     assert abs(sI.compute_delta(4096) - 1.0) < 1e-12
+
+
+def test_sharded_job_statistics_on_gpu(oracle):
+    """lgs_amd.distributed.gpu_compute (world size 1): moments, the exact d x d second
+    moments (lgs_gram) and the per-chain statistics (lgs_series_stats) of the kept
+    states equal the oracle's; covariance and R-hat follow from them."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from _oracle_shard import oracle_compute_factory
+    from conftest import golden_R, load_golden
+    from lgs_amd import _capi
+    from lgs_amd.distributed import gpu_compute, imhk_sharded
+    g = load_golden("klein_ntru32.npz")
+    R, cp, B = golden_R(g)
+    sigma = float(g["sigma"])
+    ctx = _capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    d = R.shape[0]
+    comp = gpu_compute(ctx, 4242, d, thin=2, flags=_capi.LGS_WANG_LING, want_gram=True, gr_coord=d - 1)
+    js = imhk_sharded(comp, 33, 20, rank=0, world=1)
+    ref = oracle_compute_factory(oracle, R, cp, B, sigma, 4242, thin=2, mode=oracle.IMHK_WANG_LING,
+                                 want_gram=True, gr_coord=d - 1)(0, 33, 1, 20)
+    assert js.accepts == ref.accepts and js.kept == ref.kept
+    assert np.array_equal(js.moments, ref.moments)
+    assert np.array_equal(js.gram, ref.gram)
+    np.testing.assert_allclose(js.chain_stats, ref.chain_stats, rtol=1e-12, atol=1e-9)
+    assert np.isfinite(js.gelman_rubin(10))
