@@ -32,6 +32,10 @@ def compute_tvd(samples1, samples2, bins: Optional[int] = None) -> float:
                                   "diagnostics; use bins=None (discrete samples)")
     a = _gpu.as_input(samples1)
     b = _gpu.as_input(samples2)
+    if a.shape[0] == 0 or b.shape[0] == 0:  # the reference's loop: 0.0 for two empty sets,
+        if a.shape[0] == b.shape[0]:         # ZeroDivisionError (count / 0) for one
+            return 0.0 if a.ndim == 1 else float(np.mean([0.0] * a.shape[1]))
+        raise ZeroDivisionError("division by zero")
     if str(a.dtype) != str(b.dtype):
         a = _gpu.as_input(a.astype(np.float64) if not _gpu.is_device(a) else a.double())
         b = _gpu.as_input(b.astype(np.float64) if not _gpu.is_device(b) else b.double())

@@ -167,3 +167,30 @@ def test_series_edge_cases(D):
     # max_lag beyond the series: numpy slicing keeps n lags
     x = np.arange(6, dtype=np.float64)
     np.testing.assert_allclose(D.compute_autocorrelation(x, 50), O.autocorrelation_direct(x, 50), rtol=1e-12)
+
+
+def test_reference_style_statistical_properties(D):
+    """The assertion styles of the reference's tests/unit/test_diagnostics.py on the
+    GPU drop-ins: ESS of independent draws > n/2 and above that of an AR(1) chain,
+    R-hat ~ 1 for converged chains and > 1.1 for shifted ones, TVD of a set with
+    itself exactly 0, mixing time monotone in the threshold."""
+    rng = np.random.default_rng(7)
+    n = 4000
+    iid = rng.standard_normal(n)
+    ar = np.zeros(n)
+    for i in range(1, n):
+        ar[i] = 0.9 * ar[i - 1] + np.sqrt(1 - 0.81) * rng.standard_normal()
+    ess_iid, ess_ar = D.effective_sample_size(iid), D.effective_sample_size(ar)
+    assert n * 0.5 < ess_iid <= n * 1.5 and 1 < ess_ar < ess_iid
+    conv = [rng.standard_normal(1000) for _ in range(4)]
+    shifted = [rng.standard_normal(1000) + i for i in range(4)]
+    r1, r2 = D.gelman_rubin_statistic(conv), D.gelman_rubin_statistic(shifted)
+    assert 1.0 <= r1 < 1.2 and r2 > 1.1 and r2 > r1
+    s = np.array([1, 2, 3, 1, 2, 3], dtype=np.float64)
+    assert D.compute_tvd(s, s) == 0.0
+    assert D.compute_tvd(np.ones(100), np.ones(100)) == 0.0
+    assert D.compute_tvd(np.array([]), np.array([])) == 0.0
+    with pytest.raises(ZeroDivisionError):
+        D.compute_tvd(np.array([]), np.array([1.0]))
+    tv = [0.9, 0.6, 0.4, 0.2, 0.05]
+    assert D.mixing_time_estimate(tv, 0.1) >= D.mixing_time_estimate(tv, 0.5)
