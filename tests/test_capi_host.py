@@ -107,3 +107,37 @@ def test_simple_lattice_duck_type():
     # row Gram-Schmidt: |b1| = sqrt(17), |b2*| = det / |b1|
     assert lat.min_gram_schmidt_norm == pytest.approx(min(np.sqrt(17), 11 / np.sqrt(17)))
     assert lat.smoothing_parameter() > 0
+
+
+def test_io_formats_match_reference_schema(tmp_path):
+    """Sample dumps (run_core_experiments.sage:69-73) and the scaling JSON record
+    (klein_scaling_analysis.py:322-340): same keys, npz round trip, row GS norms equal
+    to the reference's classical Gram-Schmidt loop (klein_scaling_analysis.py:113-135)."""
+    from lgs_amd import io
+    rng = np.random.default_rng(3)
+    B = rng.integers(0, 51, size=(12, 12)).astype(np.float64)
+    props = io.basis_properties(B)
+    Bs = np.zeros_like(B)
+    gs = []
+    for i in range(12):                      # the reference's loop, restated
+        Bs[i] = B[i]
+        for j in range(i):
+            Bs[i] -= np.dot(B[i], Bs[j]) / np.dot(Bs[j], Bs[j]) * Bs[j]
+        gs.append(np.linalg.norm(Bs[i]))
+    np.testing.assert_allclose(props["gs_norms"], gs, rtol=1e-9)
+    assert props["determinant"] == pytest.approx(np.linalg.det(B))
+    qm = {"x1_mean": 0.0, "x1_std": 1.0, "x1_range": [-3, 3], "mean_magnitude": 0.0,
+          "std_uniformity": 0.0, "sample_diversity": 1.0, "all_means": [0.0], "all_stds": [1.0],
+          "all_ranges": [6]}
+    rec = io.klein_scaling_record(12, B, 3.5, 0.01, 2.0, qm, 42, 1.5)
+    assert list(rec) == ["n", "determinant", "condition_number", "max_GS_norm", "sigma",
+                         "time_per_sample_ms", "quality_metrics", "seed", "additional_info"]
+    assert list(rec["additional_info"]) == ["sampling_time_total", "gs_norms", "sigma_multiplier"]
+    io.save_results_json(str(tmp_path / "Klein_LLL_n=12.json"), rec)
+    import json
+    assert json.load(open(tmp_path / "Klein_LLL_n=12.json"))["max_GS_norm"] == rec["max_GS_norm"]
+    s = rng.integers(-9, 9, size=(50, 12)).astype(np.float64)
+    io.save_samples_npz(str(tmp_path / "s.npz"), s)
+    back = io.load_samples_npz(str(tmp_path / "s.npz"))
+    assert np.array_equal(back["samples"], s)
+    np.testing.assert_allclose(back["norms"], np.linalg.norm(s, axis=1))

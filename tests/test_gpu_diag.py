@@ -194,3 +194,18 @@ def test_reference_style_statistical_properties(D):
         D.compute_tvd(np.array([]), np.array([1.0]))
     tv = [0.9, 0.6, 0.4, 0.2, 0.05]
     assert D.mixing_time_estimate(tv, 0.1) >= D.mixing_time_estimate(tv, 0.5)
+
+
+def test_sample_quality_metrics_on_gpu():
+    """klein_scaling_analysis.py:191-242 metrics from device-computed moments."""
+    from lgs_amd import io
+    rng = np.random.default_rng(12)
+    z = rng.integers(-40, 40, size=(3000, 9)).astype(np.int64)
+    z[5] = z[6]
+    m = io.sample_quality_metrics(z)
+    means, stds = np.mean(z, axis=0), np.std(z, axis=0)
+    np.testing.assert_array_equal(m["all_means"], means)
+    np.testing.assert_allclose(m["all_stds"], stds, rtol=1e-13)
+    assert m["all_ranges"] == [int(x) for x in np.ptp(z, axis=0)]
+    assert m["sample_diversity"] == len(np.unique(z.view(np.void), axis=0)) / 3000
+    assert m["x1_range"] == [int(z[:, 0].min()), int(z[:, 0].max())]
