@@ -3,8 +3,8 @@
 Workload (BASELINE.json configs[2], the config the metric is quoted on):
 NTRU n=512, q=12289 basis [[qI,0],[H,I]] (d = 1024, Philox-generated h),
 sigma = 165.7, IMHK with 2^14 chains per GPU.  One bench step = one
-``lgs_imhk`` call advancing every chain by --imhk-steps steps: 2^14 x 16 =
-2^18 Klein proposals (back-substitution + SampleZ + importance weight), the
+``lgs_imhk`` call advancing every chain by --imhk-steps steps: 2^14 x 64 =
+2^20 Klein proposals (back-substitution + SampleZ + importance weight), the
 Metropolis scan, exact integer moments, and the lattice points v = B z of every
 kept state (thin = 1), all resident in HBM.  value = Klein proposals per second
 over all ranks (weak scaling: chains per GPU fixed).
@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3_ntru512")
     ap.add_argument("--chains", type=int, default=1 << 14, help="IMHK chains per GPU")
-    ap.add_argument("--imhk-steps", type=int, default=16, help="IMHK steps per bench step")
+    ap.add_argument("--imhk-steps", type=int, default=64, help="IMHK steps per bench step (one lgs_imhk call)")
     ap.add_argument("--no-v", action="store_true", help="skip lattice points (coefficients only)")
     ap.add_argument("--exact-order", action="store_true")
     ap.add_argument("--cpu-samples", type=int, default=16384, help="IMHK proposals for the CPU baseline")

@@ -166,8 +166,6 @@ hipError_t samplez_probe(const double* mu, const double* sig, const double* u, i
                          hipStream_t st);
 hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, int zb, double* out,
                        hipStream_t st);
-hipError_t moments(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int d,
-                   unsigned long long* mom, hipStream_t st);
 // moments of the proposal store + (fsel non-null) the chains' final states into zs
 hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int64_t T,
                          const int64_t* fsel, int d, unsigned long long* mom, void* zs, int ob,
@@ -177,8 +175,6 @@ hipError_t moments_carry(const void* zs, int zb, int coord_major, int64_t nc, in
 hipError_t gather_z(const void* Z, int zb, int64_t ldz, const int64_t* sel, int64_t nq,
                     int64_t q_per_chain, const void* zs, int ob, int zs_coord_major, int64_t nc,
                     int d, void* out, int out_coord_major, hipStream_t st);
-hipError_t gather_v(const double* V, const int64_t* sel, int64_t nq, int64_t q_per_chain,
-                    const double* vs, int d, double* out, hipStream_t st);
 hipError_t transpose_out(const void* Z, int zb, int64_t ldz, int64_t n, int d, void* out, int ob,
                          hipStream_t st);
 hipError_t to_coord_major(const void* in, int ib, int64_t n, int d, void* Z, int zb, int64_t ldz,

@@ -985,39 +985,6 @@ __global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
 }
 
 // ------------------------------------------------------------ moments
-// mom[i] += sum_p cnt[p] z[i][p], mom[d+i] += sum_p cnt[p] z[i][p]^2 (int64, exact).
-template <typename ZT>
-__global__ __launch_bounds__(256) void moments_kernel(const ZT* __restrict__ Z, int64_t ldz,
-                                                      const int32_t* __restrict__ cnt, int64_t n,
-                                                      int d, int64_t chunk,
-                                                      unsigned long long* mom) {
-    const int i = blockIdx.y;
-    const int64_t p0 = (int64_t)blockIdx.x * chunk;
-    const int64_t p1 = p0 + chunk < n ? p0 + chunk : n;
-    long long s1 = 0, s2 = 0;
-    for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-        const long long w = cnt ? cnt[p] : 1;
-        const long long z = (long long)Z[(size_t)i * ldz + p];
-        s1 += w * z;
-        s2 += w * z * z;
-    }
-    __shared__ long long r1[256], r2[256];
-    r1[threadIdx.x] = s1;
-    r2[threadIdx.x] = s2;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) {
-            r1[threadIdx.x] += r1[threadIdx.x + o];
-            r2[threadIdx.x] += r2[threadIdx.x + o];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        atomicAdd(mom + i, (unsigned long long)r1[0]);
-        atomicAdd(mom + d + i, (unsigned long long)r2[0]);
-    }
-}
-
 // Moments of the retained states and the chains' final states in one pass over
 // the proposal store: mom[i] += sum_p cnt[p] z[i][p], mom[d+i] += sum_p cnt[p]
 // z[i][p]^2, and where final_sel[p / T] == p (fsel non-null) the value is also the
@@ -1157,20 +1124,6 @@ __global__ __launch_bounds__(256) void carry_cols_kernel(const OT* __restrict__ 
     if (c >= nc) return;
     const OT v = zs_coord_major ? zs[(size_t)i * nc + c] : zs[(size_t)c * d + i];
     Z[(size_t)i * ldz + col0 + c] = (ZT)v;
-}
-
-// Copy rows of V (proposal lattice points, row-major [p][d]) selected by sel;
-// sel < 0 takes the carried state's row from vs (n_chains x d).
-__global__ __launch_bounds__(256) void gather_v_kernel(const double* __restrict__ V,
-                                                       const int64_t* __restrict__ sel,
-                                                       int64_t nq, int64_t q_per_chain,
-                                                       const double* __restrict__ vs, int d,
-                                                       double* __restrict__ out) {
-    const int64_t q = blockIdx.y;
-    const int64_t s = sel[q];
-    const double* src = s >= 0 ? V + (size_t)s * d : vs + (size_t)(q / q_per_chain) * d;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < d; i += gridDim.x * blockDim.x)
-        out[(size_t)q * d + i] = src[i];
 }
 
 // Z[coord][p] (ld ldz) -> out[p][coord] (row-major n x d), 64x64 tiles via LDS.
@@ -1501,15 +1454,6 @@ hipError_t accept(const AcceptArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t moments(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int d,
-                   unsigned long long* mom, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    const int64_t chunk = 16384;
-    const dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(moments_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, d, chunk, mom));
-    return hipGetLastError();
-}
-
 hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int64_t T,
                          const int64_t* fsel, int d, unsigned long long* mom, void* zs, int ob,
                          int zs_cm, int64_t nc, hipStream_t st) {
@@ -1548,14 +1492,6 @@ hipError_t carry_cols(const void* zs, int ob, int zs_coord_major, int64_t nc, in
     if (nc <= 0) return hipSuccess;
     const dim3 grid((unsigned)((nc + 255) / 256), (unsigned)d);
     LGS_ZT(ob, OT, LGS_ZT(zb, ZT, hipLaunchKernelGGL((carry_cols_kernel<OT, ZT>), grid, dim3(256), 0, st, (const OT*)zs, zs_coord_major, nc, d, (ZT*)Z, ldz, col0)));
-    return hipGetLastError();
-}
-
-hipError_t gather_v(const double* V, const int64_t* sel, int64_t nq, int64_t q_per_chain,
-                    const double* vs, int d, double* out, hipStream_t st) {
-    if (nq <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((d + 255) / 256 < 4 ? (d + 255) / 256 : 4), (unsigned)nq);
-    hipLaunchKernelGGL(gather_v_kernel, grid, dim3(256), 0, st, V, sel, nq, q_per_chain, vs, d, out);
     return hipGetLastError();
 }
 
