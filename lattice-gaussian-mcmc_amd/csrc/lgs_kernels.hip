@@ -1365,6 +1365,9 @@ __global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z,
             const int r = r0 + wn * 64 + tn * 32 + (lane & 31);
             if (r < d) {
                 const long long v = 65536LL * p1[tn][reg] + 256LL * p2[tn][reg] + (long long)p3[tn][reg];
+#ifdef LGS_DIAG_BZ_NOSTORE  // diagnostic builds only: store cost probe
+                if (v == 0x7fffffffffffffffLL)
+#endif
                 __builtin_nontemporal_store((double)v, vrow + r);  // streamed out, not re-read
             }
         }
