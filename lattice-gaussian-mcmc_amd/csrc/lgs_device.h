@@ -32,6 +32,12 @@ struct U4 {
 
 __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                             uint32_t k0, uint32_t k1) {
+#ifndef LGS_PHILOX_HOIST
+    // opaque to loop-invariant motion: otherwise the 20 round keys of the (kernel-
+    // constant) seed are hoisted out of the coordinate loop, spilled to VGPR lanes
+    // and read back with v_readlane + s_nop at every call; recomputing them is 18 SALU adds
+    asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         if (r) {

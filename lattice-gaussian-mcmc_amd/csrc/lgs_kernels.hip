@@ -779,7 +779,10 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     if (s < rows16) {
                         const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
                         const lds_cdptr rec = (lds_cdptr)rec_lds + (i - (p_hi - 32)) * kRecStride;
-                        const double mu = (rec[kRecCp] - acc[15]) * rec[kRecIrii];
+                        // running sums rotate instead of shifting: logical acc[k] of step s
+                        // lives in acc[(k - s) & 15] (s is a compile-time constant here), so
+                        // no register moves per coordinate; 16 steps bring the map back
+                        const double mu = (rec[kRecCp] - acc[(15 - s) & 15]) * rec[kRecIrii];
                         LGS_DC_T(t_sz0);
                         const double zi = decide_coord_rec<WL>(a, i, mu, rec, rs, lw, flags, etab_s);
 #ifdef LGS_DIAG_CYCLES
@@ -802,10 +805,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                             if (!(zi <= 32639.0 && zi >= -32767.0)) flags |= kFlagOverflow16;
                         const lds_cdptr rc = rec + kRecRs;
 #pragma unroll
-                        for (int k = 0; k < 15; ++k) acc[k] = fma(rc[14 - k], zi, acc[k]);
-#pragma unroll
-                        for (int k = 15; k >= 1; --k) acc[k] = acc[k - 1];
-                        acc[0] = 0.0;
+                        for (int k = 0; k < 15; ++k) acc[(k - s) & 15] = fma(rc[14 - k], zi, acc[(k - s) & 15]);
+                        acc[(15 - s) & 15] = 0.0;  // the next step's logical acc[0]
                     }
                 }
 #pragma unroll
