@@ -1257,8 +1257,17 @@ __global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v16i_t __attribute__((ext_vector_type(16)));
 
+#ifndef LGS_BZ_OCC
+#define LGS_BZ_OCC 2
+#endif
+#ifndef LGS_BZ_TXPER
+#define LGS_BZ_TXPER 1
+#endif
+#ifndef LGS_BZ_TA
+#define LGS_BZ_TA 1
+#endif
 template <typename ZT>
-__global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z, int64_t ldz,
+__global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __restrict__ Z, int64_t ldz,
                                                     const int64_t* __restrict__ sel,
                                                     const int* __restrict__ kchunk,
                                                     const int* __restrict__ koff,
@@ -1267,7 +1276,9 @@ __global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z,
                                                     int64_t n, double* __restrict__ V, int64_t ldv,
                                                     int64_t rb, int64_t rstride, int64_t roff,
                                                     unsigned int* flags, int tx_count, int64_t ty_count) {
-    constexpr int BM = 64, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
+    constexpr int TA = LGS_BZ_TA;  // 32-sample MFMA tiles per wave
+    constexpr int BM = 64 * TA, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
+    constexpr int KPT = KC * BM / 256;  // coefficients per thread per chunk
     __shared__ __attribute__((aligned(16))) int8_t Zs1[BM * P], Zs0[BM * P], Bs1[BN * P], Bs0[BN * P];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
@@ -1275,50 +1286,68 @@ __global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z,
     // workgroup b runs on XCD b % 8; the tx_count coordinate tiles of one sample
     // tile are given to consecutive workgroups of the same XCD, which then reads
     // that sample tile's coefficients from HBM once and from its own L2 after.
+    // Each workgroup computes LGS_BZ_TXPER consecutive coordinate tiles of its
+    // sample tile, so the output stores of one tile drain while the MFMAs of the
+    // next one run.
     const int64_t b = blockIdx.x, w = b >> 3;
     const int64_t ty = (w / tx_count) * 8 + (b & 7);
-    const int tx = (int)(w % tx_count);
+    const int txg = (int)(w % tx_count);
     if (ty >= ty_count) return;
-    const int r0 = tx * BN;
     const int64_t s0 = ty * BM;
-    v16i_t p1[2], p2[2], p3[2];
+    const int ntx = (d + BN - 1) / BN;
+    ZT zmax = 0, zmin = 0;  // range of the coefficients read (exactness check)
+    for (int tx = txg * LGS_BZ_TXPER; tx < ntx && tx < (txg + 1) * LGS_BZ_TXPER; ++tx) {
+    const int r0 = tx * BN;
+    v16i_t p1[TA][2], p2[TA][2], p3[TA][2];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        p1[t] = (v16i_t){};
-        p2[t] = (v16i_t){};
-        p3[t] = (v16i_t){};
-    }
-    bool bad = false;
-    const int zm = tid & 63, zq = tid >> 6;
+    for (int ta = 0; ta < TA; ++ta)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            p1[ta][t] = (v16i_t){};
+            p2[ta][t] = (v16i_t){};
+            p3[ta][t] = (v16i_t){};
+        }
+    const int zm = tid & (BM - 1), zq = tid / BM;
     const int64_t zs_ = s0 + zm;
     const int64_t zcol = zs_ < n ? (sel ? sel[zs_] : zs_) : 0;  // this thread's sample column
     // only the K chunks where this row tile of B has a non-zero digit (exact skip)
-    const int ci0 = koff[tx], ci1 = koff[tx + 1];
+    const int ci0 = koff[tx];
+#ifdef LGS_DIAG_BZ_NOMFMA  // diagnostic builds only: epilogue cost probe
+    const int ci1 = ci0;
+#else
+    const int ci1 = koff[tx + 1];
+#endif
     for (int ci = ci0; ci < ci1; ++ci) {
         const int c0 = kchunk[ci] * KC;
         {  // z chunk -> balanced base-256 digits, [sample][k] byte planes
             const bool sok = zs_ < n;
-            const ZT* zp = Z + (size_t)(c0 + zq * 16) * ldz + zcol;
+            const ZT* zp = Z + (size_t)(c0 + zq * KPT) * ldz + zcol;
+#pragma unroll
+            for (int h = 0; h < KPT / 16; ++h) {
             v4i_t w0, w1;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                unsigned int lo4 = 0, hi4 = 0;
+                // z = 256 hi + lo with lo in [-128, 127]: lo's byte is z's low
+                // byte and hi = (z + 128) >> 8, whose byte is byte 1 of z + 128;
+                // v_perm_b32 gathers four such bytes into one dword
+                unsigned int zz[4], hh[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int c = c0 + zq * 16 + q * 4 + j;
-                    const ZT zr = (sok && c < d) ? zp[(size_t)(q * 4 + j) * ldz] : (ZT)0;
-                    bad |= (zr > (ZT)32639) | (zr < (ZT)-32639);
-                    const int z = (int)zr;
-                    const int lo = (z << 24) >> 24;  // balanced low digit in [-128, 127]
-                    const int hi = (z - lo) >> 8;
-                    lo4 |= ((unsigned int)lo & 0xffu) << (8 * j);
-                    hi4 |= ((unsigned int)hi & 0xffu) << (8 * j);
+                    const int c = c0 + zq * KPT + h * 16 + q * 4 + j;
+                    const ZT zr = (sok && c < d) ? zp[(size_t)(h * 16 + q * 4 + j) * ldz] : (ZT)0;
+                    zmax = max(zmax, zr);
+                    zmin = min(zmin, zr);
+                    zz[j] = (unsigned int)(int)zr;
+                    hh[j] = zz[j] + 128u;
                 }
-                w0[q] = (int)lo4;
-                w1[q] = (int)hi4;
+                w0[q] = (int)(__builtin_amdgcn_perm(zz[1], zz[0], 0x0c0c0400u) |
+                              __builtin_amdgcn_perm(zz[3], zz[2], 0x04000c0cu));
+                w1[q] = (int)(__builtin_amdgcn_perm(hh[1], hh[0], 0x0c0c0501u) |
+                              __builtin_amdgcn_perm(hh[3], hh[2], 0x05010c0cu));
             }
-            *(v4i_t*)&Zs0[zm * P + zq * 16] = w0;
-            *(v4i_t*)&Zs1[zm * P + zq * 16] = w1;
+            *(v4i_t*)&Zs0[zm * P + zq * KPT + h * 16] = w0;
+            *(v4i_t*)&Zs1[zm * P + zq * KPT + h * 16] = w1;
+            }
         }
 #pragma unroll
         for (int e = 0; e < 2; ++e) {  // B digit planes [coord][k], 16 B per thread per plane
@@ -1332,48 +1361,87 @@ __global__ __launch_bounds__(256, 2) void bz_i8_kernel(const ZT* __restrict__ Z,
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int kb = ks * 32 + 16 * (lane >> 5);
-            const int arow = wm * 32 + (lane & 31);
-            const v4i_t a1 = *(const v4i_t*)&Zs1[arow * P + kb];
-            const v4i_t a0 = *(const v4i_t*)&Zs0[arow * P + kb];
+            v4i_t a1[TA], a0[TA];
+#pragma unroll
+            for (int ta = 0; ta < TA; ++ta) {
+                const int arow = (wm * TA + ta) * 32 + (lane & 31);
+                a1[ta] = *(const v4i_t*)&Zs1[arow * P + kb];
+                a0[ta] = *(const v4i_t*)&Zs0[arow * P + kb];
+            }
 #pragma unroll
             for (int tn = 0; tn < 2; ++tn) {
                 const int col = wn * 64 + tn * 32 + (lane & 31);
                 const v4i_t b1 = *(const v4i_t*)&Bs1[col * P + kb];
                 const v4i_t b0 = *(const v4i_t*)&Bs0[col * P + kb];
-                p1[tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, p1[tn], 0, 0, 0);
-                p2[tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, p2[tn], 0, 0, 0);
-                p2[tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, p2[tn], 0, 0, 0);
-                p3[tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, p3[tn], 0, 0, 0);
+#pragma unroll
+                for (int ta = 0; ta < TA; ++ta) {
+                    p1[ta][tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[ta], b1, p1[ta][tn], 0, 0, 0);
+                    p2[ta][tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[ta], b0, p2[ta][tn], 0, 0, 0);
+                    p2[ta][tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[ta], b1, p2[ta][tn], 0, 0, 0);
+                    p3[ta][tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[ta], b0, p3[ta][tn], 0, 0, 0);
+                }
             }
         }
         __syncthreads();
     }
-    // output rows: sample q -> (q / rb) * rstride + roff + q % rb, in 32-bit pieces
-    const int64_t qb = s0 + wm * 32;
+    // output rows: sample q -> (q / rb) * rstride + roff + q % rb.  The wave's 32
+    // rows start at qb (wave-uniform); with rb >= 32 they cross at most one block
+    // boundary, so each row's address is a uniform base + row * ldv + (one
+    // uniform jump past the boundary) -- no per-row division or 64-bit multiply.
+    // v = 65536 p1 + 256 p2 + p3 is formed in fp64: every partial sum is an
+    // integer below 2^53, so it is exact (and equal to the int64 combination).
+    const int lrow = 4 * (lane >> 5);
+#pragma unroll
+    for (int ta = 0; ta < TA; ++ta) {
+    const int64_t qb = s0 + (wm * TA + ta) * 32;
     const int64_t cb = qb / rb;
-    const unsigned int kb0 = (unsigned int)(qb - cb * rb), urb = (unsigned int)rb;
+    const int64_t kb0 = qb - cb * rb;
+    const int nrow = (int)min<int64_t>(n - qb, 32);  // valid rows of this tile
+    if (rb >= 32) {
+        const int wrap_row = (int)min<int64_t>(rb - kb0, 32);  // first row past the boundary
+        double* const vbase = V + (size_t)(cb * rstride + roff + kb0) * ldv + r0 + wn * 64 + (lane & 31);
+        const int64_t jump = (rstride - rb) * ldv;
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
-        const int64_t s = qb + row;
-        if (s >= n) continue;
-        const unsigned int kk = kb0 + (unsigned int)row;
-        const unsigned int wrap = kk / urb;
-        const int64_t orow = (cb + wrap) * rstride + roff + (kk - wrap * urb);
-        double* vrow = V + (size_t)orow * ldv;
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = (reg & 3) + 8 * (reg >> 2) + lrow;
+            if (row >= nrow) continue;
+            double* vrow = vbase + (size_t)row * ldv + (row >= wrap_row ? jump : 0);
 #pragma unroll
-        for (int tn = 0; tn < 2; ++tn) {
-            const int r = r0 + wn * 64 + tn * 32 + (lane & 31);
-            if (r < d) {
-                const long long v = 65536LL * p1[tn][reg] + 256LL * p2[tn][reg] + (long long)p3[tn][reg];
+            for (int tn = 0; tn < 2; ++tn) {
+                if (r0 + wn * 64 + tn * 32 + (lane & 31) < d) {
+                    const double v = fma((double)p1[ta][tn][reg], 65536.0, (double)p2[ta][tn][reg] * 256.0) +
+                                     (double)p3[ta][tn][reg];
 #ifdef LGS_DIAG_BZ_NOSTORE  // diagnostic builds only: store cost probe
-                if (v == 0x7fffffffffffffffLL)
+                    if (v == 0.5)
 #endif
-                __builtin_nontemporal_store((double)v, vrow + r);  // streamed out, not re-read
+                    __builtin_nontemporal_store(v, vrow + tn * 32);  // streamed out, not re-read
+                }
+            }
+        }
+    } else {
+        const unsigned int ukb0 = (unsigned int)kb0, urb = (unsigned int)rb;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = (reg & 3) + 8 * (reg >> 2) + lrow;
+            if (row >= nrow) continue;
+            const unsigned int kk = ukb0 + (unsigned int)row;
+            const unsigned int wrap = kk / urb;
+            const int64_t orow = (cb + wrap) * rstride + roff + (kk - wrap * urb);
+            double* vrow = V + (size_t)orow * ldv;
+#pragma unroll
+            for (int tn = 0; tn < 2; ++tn) {
+                const int r = r0 + wn * 64 + tn * 32 + (lane & 31);
+                if (r < d) {
+                    const double v = fma((double)p1[ta][tn][reg], 65536.0, (double)p2[ta][tn][reg] * 256.0) +
+                                     (double)p3[ta][tn][reg];
+                    __builtin_nontemporal_store(v, vrow + r);
+                }
             }
         }
     }
-    if (bad) atomicOr(flags, kFlagI8Range);
+    }
+    }
+    if (zmax > (ZT)32639 || zmin < (ZT)-32639) atomicOr(flags, kFlagI8Range);
 }
 
 // ============================================================ launchers
@@ -1558,8 +1626,8 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    const int tx = (d + 127) / 128;
-    const int64_t ty = (n + 63) / 64;
+    const int tx = ((d + 127) / 128 + LGS_BZ_TXPER - 1) / LGS_BZ_TXPER;  // coordinate-tile groups
+    const int64_t ty = (n + 64 * LGS_BZ_TA - 1) / (64 * LGS_BZ_TA);
     const dim3 grid((unsigned)(tx * ((ty + 7) / 8) * 8));  // whole rounds of 8 XCDs (extra tiles exit)
     LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty));
     return hipGetLastError();

@@ -11,10 +11,9 @@ P3="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32 SQ_IN
 P4="SQ_INSTS_SMEM SQ_INST_CYCLES_SMEM SQ_INST_LEVEL_SMEM SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM"
 for v in ${SQ_VARIANTS:-"main:lattice-gaussian-mcmc_amd/lgs_amd/_lib/liblgs_hip.so nosz:lattice-gaussian-mcmc_amd/build/var/nosz.so"}; do
   name=${v%%:*}; lib=$R/${v#*:}
-  i=0
-  for P in "$P1" "$P2" "$P3" "$P4"; do
-    i=$((i+1))
-    LGS_LIB=$lib timeout -k 10 300 rocprofv3 --pmc $P -d $OUT/$name/p$i -o run --output-format csv -- python3 $R/tools/kbench.py --one --reps 1 > $OUT/$name.p$i.log 2>&1 || { tail -20 $OUT/$name.p$i.log; exit 1; }
+  for i in ${SQ_SEL:-1 2 3 4}; do
+    eval P=\$P$i
+    LGS_LIB=$lib timeout -k 10 300 rocprofv3 --pmc $P -d $OUT/$name/p$i -o run --output-format csv -- python3 $R/tools/kbench.py --one --reps 1 ${KB_ARGS} > $OUT/$name.p$i.log 2>&1 || { tail -20 $OUT/$name.p$i.log; exit 1; }
   done
 done
-python3 $R/tools/sq_summary.py $OUT
+python3 $R/tools/sq_summary.py $OUT ${SQ_KERNEL:-klein}

@@ -29,7 +29,8 @@ def run_one(args):
     z = torch.empty((d, n), dtype=torch.int32, device="cuda:0")
     lw = torch.empty(n, dtype=torch.float64, device="cuda:0")
     flags = _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR | (_capi.LGS_EXACT_ORDER if args.exact else 0)
-    ctx.klein(1, 0, n, z, None, lw, flags)
+    v = torch.empty((n, d), dtype=torch.float64, device="cuda:0") if args.bz else None
+    ctx.klein(1, 0, n, z, v, lw, flags)
     import ctypes
     diag = getattr(_capi.load_library(), "lgs_diag_cycles_read", None)
     dbuf = (ctypes.c_ulonglong * 16)()
@@ -37,11 +38,15 @@ def run_one(args):
         diag(dbuf)  # reset after the warm-up launch
     ctx.timing_enable(True)
     for r in range(args.reps):
-        ctx.klein(1, (r + 1) * n, n, z, None, lw, flags)
+        ctx.klein(1, (r + 1) * n, n, z, v, lw, flags)
     ms, k = ctx.timing_get(_capi.KERNEL_KLEIN)
     avg = ms / k
     out = {"lib": os.environ.get("LGS_LIB", "default"), "config": args.config, "d": d, "n": n,
            "kernel_ms": round(avg, 3), "samples_per_s": round(n / avg * 1e3, 1)}
+    if args.bz:
+        ms, k = ctx.timing_get(_capi.KERNEL_BZ)
+        out["bz_ms"] = round(ms / k, 3)
+        out["bz_write_GBps"] = round(n * d * 8 / (ms / k) * 1e-6, 1)
     if diag is not None:
         diag(dbuf)
         waves = args.reps * n // 64
@@ -61,6 +66,7 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--exact", action="store_true")
     ap.add_argument("--one", action="store_true")
+    ap.add_argument("--bz", action="store_true", help="also compute v = Bz and time bz_i8")
     args = ap.parse_args()
     libs = os.environ.get("LGS_LIBS")
     if args.one or not libs:

@@ -6,13 +6,14 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1]
+kname = sys.argv[2] if len(sys.argv) > 2 else "klein"
 for var in sorted(os.listdir(root)):
     d = os.path.join(root, var)
     if not os.path.isdir(d):
         continue
     tot = defaultdict(float)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        rows = [r for r in csv.DictReader(open(f)) if "klein" in r.get("Kernel_Name", "")]
+        rows = [r for r in csv.DictReader(open(f)) if kname in r.get("Kernel_Name", "")]
         if not rows:
             continue
         # last dispatch of the Klein kernel (the timed rep)
