@@ -1,0 +1,115 @@
+"""GPU edge cases of the Klein / IMHK path (empty and ragged inputs).
+
+* Ragged shapes: lattice dimensions that are not multiples of the 16/32-row
+  panels or the 64/128-wide B z tiles (d = 1, 2, 31, 33, 65, 100) and sample
+  counts that are not multiples of the 64-lane wave; z and the integer lattice
+  points v are bit-exact against the oracle in both kernel orders.
+* Empty inputs: n = 0 Klein calls, IMHK with zero chains or zero steps, and
+  zero-vector moments / decodes are no-ops that leave the outputs untouched.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MODES = {"exact": 2, "panel": 0}  # LGS_EXACT_ORDER = 0x2
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from lgs_amd import _capi
+    return _capi
+
+
+@pytest.fixture(scope="module")
+def ctx(capi):
+    return capi.Context(0)
+
+
+def _int_basis(d, seed):
+    """Well-conditioned integer basis: 6 I plus three +-1 entries per row."""
+    rng = np.random.default_rng(seed)
+    B = 6 * np.eye(d)
+    for i in range(d):
+        B[i, rng.integers(0, d, 3)] += rng.choice([-1.0, 1.0], 3)
+    return B
+
+
+def _ill_basis(d, seed):
+    """Integer basis L U with unit-ish triangles: condition number ~1e15, so the
+    coefficients grow to ~2^50 and ulp(mu) approaches the integer spacing."""
+    rng = np.random.default_rng(seed)
+    L = np.tril(rng.integers(-2, 3, (d, d)), -1) + np.diag(rng.integers(1, 4, d))
+    U = np.triu(rng.integers(-2, 3, (d, d)), 1) + np.eye(d, dtype=np.int64)
+    return (L @ U).astype(np.float64)
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("d,n", [(1, 1), (2, 65), (31, 130), (33, 63), (65, 129), (100, 200)])
+def test_klein_ragged_shapes_vs_oracle(ctx, oracle, d, n, mode):
+    B = _int_basis(d, d)
+    R, cp = oracle.qr_prepare(B)
+    sigma = 8.0
+    ctx.set_basis(R, cp, B, sigma)
+    r = ctx.klein_host(777 + d, 31, n, want_z=True, want_v=True, flags=MODES[mode])
+    o = oracle.klein(R, cp, sigma, n, seed=777 + d, first_sample=31, B=B)
+    assert r["z"].shape == (n, d)
+    assert np.array_equal(r["z"], o["z"])
+    assert np.array_equal(r["v"], o["v"])
+
+
+def test_exact_order_on_ill_conditioned_basis(ctx, oracle):
+    """LGS_EXACT_ORDER keeps the reference's sequential fp64 order, so it stays
+    bit-exact even where |mu| ~ 2^50 and the blocked default order's ulp-level
+    differences in mu change many decisions."""
+    B = _ill_basis(64, 64)
+    R, cp = oracle.qr_prepare(B)
+    ctx.set_basis(R, cp, B, 3.5)
+    r = ctx.klein_host(841, 31, 128, want_z=True, want_v=True, flags=MODES["exact"])
+    o = oracle.klein(R, cp, 3.5, 128, seed=841, first_sample=31, B=B)
+    assert np.abs(o["z"]).max() > 1 << 40
+    assert np.array_equal(r["z"], o["z"])
+
+
+def test_klein_empty(ctx, oracle, capi):
+    B = _int_basis(33, 1)
+    R, cp = oracle.qr_prepare(B)
+    ctx.set_basis(R, cp, B, 2.0)
+    r = ctx.klein_host(5, 0, 0, want_z=True, want_v=True, want_logw=True)
+    assert r["z"].shape == (0, 33) and r["v"].shape == (0, 33) and r["logw"].shape == (0,)
+    ctx.klein(5, 0, 0, None, None, None, 0)  # nothing requested, nothing done
+
+
+def test_imhk_zero_steps_and_zero_chains(ctx, oracle, capi):
+    B = _int_basis(33, 2)
+    R, cp = oracle.qr_prepare(B)
+    ctx.set_basis(R, cp, B, 2.0)
+    nc, d = 70, 33
+    z = np.zeros((nc, d), dtype=np.int32)
+    lw = np.zeros(nc)
+    init = np.zeros(nc, dtype=np.int32)
+    acc = np.zeros(nc, dtype=np.int64)
+    ctx.imhk(9, 0, nc, 1, 3, 1, z, lw, init, acc, flags=capi.LGS_WANG_LING)
+    assert init.all()
+    z0, lw0, acc0 = z.copy(), lw.copy(), acc.copy()
+    mom = np.zeros(2 * d, dtype=np.int64)
+    ctx.imhk(9, 0, nc, 4, 0, 1, z, lw, init, acc, moments=mom, flags=capi.LGS_WANG_LING)
+    assert np.array_equal(z, z0) and np.array_equal(lw, lw0) and np.array_equal(acc, acc0)
+    assert not mom.any()
+    e = np.zeros((0, d), dtype=np.int32)
+    ctx.imhk(9, 0, 0, 1, 5, 1, e, np.zeros(0), np.zeros(0, dtype=np.int32), np.zeros(0, dtype=np.int64),
+             moments=mom, flags=capi.LGS_WANG_LING)
+    assert not mom.any()
+
+
+def test_zero_vector_reductions_and_decodes(ctx, oracle):
+    from lgs_amd import diagnostics
+    B = _int_basis(17, 3)
+    R, cp = oracle.qr_prepare(B)
+    ctx.set_basis(R, cp, B, 2.0)
+    s = np.full(17, 7, dtype=np.int64)
+    G = np.full((17, 17), 3, dtype=np.int64)
+    ctx.gram(np.zeros((0, 17), dtype=np.int32), sum_out=s, gram_out=G)
+    assert (s == 7).all() and (G == 3).all()
+    s2, G2 = diagnostics.gram(np.zeros((0, 17), dtype=np.int32))
+    assert not s2.any() and not G2.any()
