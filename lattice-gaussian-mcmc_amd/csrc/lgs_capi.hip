@@ -112,7 +112,7 @@ struct lgs_ctx {
     DevBuf Z, LW, V, sel, fsel, cnt, ccnt, flags, stage_a, stage_b, stage_c, stage_d, stage_e,
         stage_f, stage_g, vs;
     int64_t max_props = 1 << 18;
-    int zint = 4;  // internal coefficient store width (bytes); LGS_ZINT=2: 16-bit, sticky 32-bit on overflow
+    int zint = 2;  // internal coefficient store width (bytes): 16-bit, sticky 32-bit on overflow; LGS_ZINT=4 forces 32-bit
     // timing
     bool timing = false;
     double t_ms[6] = {0, 0, 0, 0, 0, 0};
@@ -914,6 +914,21 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
             }
         HIP_TRY(hipMemcpyAsync(lws, cur.data(), nc * 8, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(init, h_init.data(), nc * 4, hipMemcpyHostToDevice, c->stream));
+    }
+
+    // ---- a 16-bit proposal store receives the chain states through carry_cols:
+    // states that do not fit (caller-supplied ones) switch this context to 32 bits
+    if (zb == 2 && carry && n_steps > 0) {
+        HIP_TRY(lgs::launch::check_range16(zs, ob, nc * d, c->flags.as<unsigned int>(), c->stream));
+        unsigned int f = 0;
+        HIP_TRY(hipMemcpyAsync(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (f & lgs::kFlagOverflow16) {
+            f &= ~lgs::kFlagOverflow16;
+            HIP_TRY(hipMemcpy(c->flags.p, &f, sizeof(f), hipMemcpyHostToDevice));
+            c->zint = 4;
+            zb = 4;
+        }
     }
 
     // ---- blocks

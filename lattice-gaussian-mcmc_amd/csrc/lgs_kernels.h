@@ -196,6 +196,7 @@ hipError_t nearest_plane(int d, int64_t n, int panel, const double* RP, const do
                          unsigned int* flags, hipStream_t st);
 hipError_t round_coeffs(const double* W, int64_t ldw, int d, int64_t n, int zb, void* Z, int64_t ldz,
                         unsigned int* flags, hipStream_t st);
+hipError_t check_range16(const void* zs, int ob, int64_t count, unsigned int* flags, hipStream_t st);
 hipError_t carry_cols(const void* zs, int ob, int zs_coord_major, int64_t nc, int d, void* Z, int zb,
                       int64_t ldz, int64_t col0, hipStream_t st);
 }  // namespace launch

@@ -1114,6 +1114,18 @@ __global__ __launch_bounds__(256) void gather_z_kernel(const ZT* __restrict__ Z,
         out[(size_t)q * d + i] = v;
 }
 
+// Sets kFlagOverflow16 when a coefficient does not fit a 16-bit store (the chain
+// states a 16-bit proposal store receives through carry_cols).
+template <typename OT>
+__global__ __launch_bounds__(256) void range16_kernel(const OT* __restrict__ zs, int64_t count,
+                                                      unsigned int* flags) {
+    bool out = false;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < count;
+         e += (int64_t)gridDim.x * blockDim.x)
+        out |= zs[e] > (OT)32767 || zs[e] < (OT)-32768;
+    if (out) atomicOr(flags, kFlagOverflow16);
+}
+
 // Chain states (caller layout, width OT) into columns col0 .. col0+nc-1 of the
 // coordinate-major proposal store, so kept-state selections are plain columns.
 template <typename OT, typename ZT>
@@ -1556,6 +1568,13 @@ hipError_t gather_z(const void* Z, int zb, int64_t ldz, const int64_t* sel, int6
     if (nq <= 0) return hipSuccess;
     const dim3 grid((unsigned)((nq + 255) / 256), (unsigned)d);
     LGS_ZT(zb, ZT, LGS_ZT(ob, OT, hipLaunchKernelGGL((gather_z_kernel<ZT, OT>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, nq, q_per_chain, (const OT*)zs, zs_coord_major, nc, d, (OT*)out, out_coord_major)));
+    return hipGetLastError();
+}
+
+hipError_t check_range16(const void* zs, int ob, int64_t count, unsigned int* flags, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    const dim3 grid((unsigned)std::min<int64_t>((count + 255) / 256, 2048));
+    LGS_ZT(ob, OT, hipLaunchKernelGGL(range16_kernel<OT>, grid, dim3(256), 0, st, (const OT*)zs, count, flags));
     return hipGetLastError();
 }
 

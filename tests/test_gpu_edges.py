@@ -113,3 +113,42 @@ def test_zero_vector_reductions_and_decodes(ctx, oracle):
     assert (s == 7).all() and (G == 3).all()
     s2, G2 = diagnostics.gram(np.zeros((0, 17), dtype=np.int32))
     assert not s2.any() and not G2.any()
+
+
+def test_imhk_16bit_store_with_wide_carried_states(capi, oracle):
+    """The default 16-bit proposal store receives the chain states through the carry
+    columns; caller-supplied states beyond int16 switch it to 32 bits, so lattice
+    points, moments and final states are those of a 32-bit store (LGS_ZINT=4)."""
+    import os
+
+    import torch
+    d, nc, T = 40, 64, 6
+    B = _int_basis(d, 5)
+    R, cp = oracle.qr_prepare(B)
+    z0 = np.random.default_rng(1).integers(-5, 6, (nc, d)).astype(np.int32)
+    z0[:, 0] = 50000
+    z0[3, 5] = -70000
+    for zint in ("2", "4"):
+        os.environ["LGS_ZINT"] = zint
+        try:
+            c = capi.Context(0)
+        finally:
+            del os.environ["LGS_ZINT"]
+        c.set_basis(R, cp, B, 3.0)
+        dev = "cuda:0"
+        z = torch.from_numpy(z0.copy()).to(dev)
+        lw = torch.full((nc,), 1e6, dtype=torch.float64, device=dev)  # no proposal reaches it
+        init = torch.ones(nc, dtype=torch.int32, device=dev)
+        acc = torch.zeros(nc, dtype=torch.int64, device=dev)
+        vs = torch.zeros((nc, T, d), dtype=torch.float64, device=dev)
+        mom = torch.zeros(2 * d, dtype=torch.int64, device=dev)
+        c.imhk(3, 0, nc, 1, T, 1, z, lw, init, acc, v_samples=vs, moments=mom,
+               flags=capi.LGS_DEVICE_PTRS | capi.LGS_WANG_LING)
+        assert not acc.cpu().numpy().any()
+        assert np.array_equal(z.cpu().numpy(), z0)
+        v0 = z0.astype(np.float64) @ B.T
+        assert np.array_equal(vs.cpu().numpy(), np.repeat(v0[:, None, :], T, axis=1))
+        zz = z0.astype(np.int64)
+        m = mom.cpu().numpy()
+        assert np.array_equal(m[:d], T * zz.sum(0))
+        assert np.array_equal(m[d:], T * (zz * zz).sum(0))
