@@ -991,8 +991,8 @@ __global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
 // z[i][p]^2, and where final_sel[p / T] == p (fsel non-null) the value is also the
 // chain's new state, written to z_state in the caller's layout -- the final-state
 // gather folded into the pass that already reads every proposal (a separate
-// gather touches one proposal in T per cache line).  VEC: four consecutive
-// proposals per lane in one 8/16/32-byte load (ldz % 4 == 0, n % 4 == 0).
+// gather touches one proposal in T per cache line).  VEC: 8 (16-bit store) or 4
+// consecutive proposals per lane in one load (ldz and n multiples of that).
 template <typename ZT, typename OT, bool VEC>
 __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict__ Z, int64_t ldz,
                                                             const int32_t* __restrict__ cnt, int64_t n,
@@ -1012,18 +1012,42 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
             zs[(size_t)c * d + i] = (OT)z;
     };
     if constexpr (VEC) {
-        typedef ZT zv4_t __attribute__((ext_vector_type(4)));
+        // VW consecutive proposals per lane in one 16-byte load (8 for a 16-bit store)
+        constexpr int VW = sizeof(ZT) == 2 ? 8 : 4;
+        typedef ZT zv_t __attribute__((ext_vector_type(VW)));
         typedef int iv4_t __attribute__((ext_vector_type(4)));
-        for (int64_t p = p0 + 4 * (int64_t)threadIdx.x; p < p1; p += 1024) {
-            const zv4_t zv = *(const zv4_t*)(zr + p);
-            const iv4_t wv = cnt ? *(const iv4_t*)(cnt + p) : (iv4_t){1, 1, 1, 1};
-            const long long z0 = zv[0], z1 = zv[1], z2 = zv[2], z3 = zv[3];
-            s1 += wv[0] * z0 + wv[1] * z1 + wv[2] * z2 + wv[3] * z3;
-            s2 += wv[0] * z0 * z0 + wv[1] * z1 * z1 + wv[2] * z2 * z2 + wv[3] * z3 * z3;
-            if (fsel) {  // chains whose proposals touch [p, p+3] (one, two at a boundary)
-                for (uint32_t c = (uint32_t)p / (uint32_t)T; (int64_t)c * T <= p + 3 && (int64_t)c < nc; ++c) {
+        const double rT = 1.0 / (double)T;
+        for (int64_t p = p0 + VW * (int64_t)threadIdx.x; p < p1; p += VW * 256) {
+            const zv_t zv = *(const zv_t*)(zr + p);
+            int w[VW];
+#pragma unroll
+            for (int g = 0; g < VW / 4; ++g) {
+                const iv4_t wv = cnt ? *(const iv4_t*)(cnt + p + 4 * g) : (iv4_t){1, 1, 1, 1};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) w[4 * g + k] = wv[k];
+            }
+#pragma unroll
+            for (int k = 0; k < VW; ++k) {
+                if constexpr (sizeof(ZT) == 2) {  // z^2 < 2^30: one 32x32->64 multiply-add each
+                    const int z = zv[k];
+                    s1 += (long long)w[k] * z;
+                    s2 += (long long)w[k] * (z * z);
+                } else {
+                    const long long z = zv[k];
+                    s1 += w[k] * z;
+                    s2 += w[k] * z * z;
+                }
+            }
+            if (fsel) {  // chains whose proposals touch [p, p + VW - 1] (one, two at a boundary)
+                // p / T through the fp64 reciprocal, corrected by one step (p < 2^32)
+                int64_t c = (int64_t)((double)p * rT);
+                const int64_t rem = p - c * T;
+                c += rem < 0 ? -1 : (rem >= T ? 1 : 0);
+                for (; c * T <= p + VW - 1 && c < nc; ++c) {
                     const int64_t k = fsel[c] - p;
-                    if (k >= 0 && k < 4) put(c, k == 0 ? z0 : k == 1 ? z1 : k == 2 ? z2 : z3);
+#pragma unroll
+                    for (int e = 0; e < VW; ++e)
+                        if (k == e) put(c, (long long)zv[e]);
                 }
             }
         }
@@ -1544,7 +1568,8 @@ hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt,
     if (n <= 0) return hipSuccess;
     const int64_t chunk = 16384;  // multiple of 4
     const dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
-    const bool vec = ldz % 4 == 0 && n % 4 == 0 && ((uintptr_t)Z % (4 * (uintptr_t)zb)) == 0 &&
+    const int vw = zb == 2 ? 8 : 4;  // proposals per lane of the vector path
+    const bool vec = ldz % vw == 0 && n % vw == 0 && ((uintptr_t)Z % (vw * (uintptr_t)zb)) == 0 &&
                      (!cnt || ((uintptr_t)cnt % 16) == 0);
     LGS_ZT(zb, ZT, LGS_ZT(ob, OT, {
         if (vec)

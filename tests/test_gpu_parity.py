@@ -522,7 +522,7 @@ def test_imhk_device_v_samples(ctx, capi):
 @pytest.mark.parametrize("nc,steps,cm", [(64, 12, True), (37, 7, True), (40, 9, False)])
 def test_imhk_fused_final_state_with_moments(ctx, capi, oracle, nc, steps, cm):
     """Moments + lattice points (carry columns) take the fused moments/final-state
-    pass (vectorised when the store is 4-aligned, scalar otherwise); Wang-Ling
+    pass (vectorised when the store is 8-aligned -- 16-bit store, 8 proposals per lane, chain boundaries inside a vector -- scalar otherwise); Wang-Ling
     weights make chains reject, so some chains keep their carried-in state.
     Final states, moments and acceptances equal the oracle's."""
     import torch
