@@ -99,6 +99,12 @@ struct lgs_ctx {
     DevBuf RD, RDOFF;             // int8-digit far field: R digit fragments, panel offsets
     bool has_rd = false, oz_off = false;  // oz_off: a |z| > 32767 was seen (sticky)
     DevBuf H16, F0;               // int8-digit far field scratch: coefficient history, tile-0 sums
+    // the last Klein launch's history, valid for columns [0, cols) of the store Z it
+    // wrote (B z reads its digits from there); reset by every Klein launch
+    struct {
+        const void* Z = nullptr;
+        int64_t lanes = 0, cols = 0;
+    } hist;
     DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
     DevBuf kchunk, koff;          // per 128-row tile of B: the 64-column chunks with a non-zero digit
     DevBuf etab;                  // SampleZ erf/exp table (lgs_device.h erf_gauss)
@@ -257,6 +263,7 @@ int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int zb, void* 
     static const char* force = getenv("LGS_KERNEL");
     int kernel = lgs::kKernelValu;
     used_oz = false;
+    c->hist.Z = nullptr;
     if (exact || (force && strcmp(force, "exact") == 0))
         kernel = lgs::kKernelExact;
     else if (!(force && strcmp(force, "valu") == 0) && a.n % 64 == 0 && a.ldz % 4 == 0 &&
@@ -294,7 +301,14 @@ int run_klein_store(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int& zb,
     HIP_TRY(hipStreamSynchronize(c->stream));
     unsigned int f = 0;
     HIP_TRY(hipMemcpy(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost));
-    if (!(f & lgs::kFlagOverflow16)) return LGS_OK;
+    if (!(f & lgs::kFlagOverflow16)) {
+        if (oz) {
+            c->hist.Z = Z;
+            c->hist.lanes = (a.n + 63) / 64 * 64;
+            c->hist.cols = a.n;
+        }
+        return LGS_OK;
+    }
     f &= ~lgs::kFlagOverflow16;
     HIP_TRY(hipMemcpy(c->flags.p, &f, sizeof(f), hipMemcpyHostToDevice));
     if (zb == 2) {
@@ -314,8 +328,11 @@ int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
 
 // v = B z: exact int8-digit MFMA kernel for integer bases (fp64 replay on digit
 // overflow, see finish()), fp64 MFMA kernel otherwise.  LGS_BZ_FP64=1 forces fp64.
+// after_klein: Z holds the output of the last Klein launch (its int16 history is
+// then a valid source of the digits for the columns that launch wrote).
 int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
-           int64_t rb = 0, int64_t rstride = 0, int64_t roff = 0, const int64_t* sel = nullptr) {
+           int64_t rb = 0, int64_t rstride = 0, int64_t roff = 0, const int64_t* sel = nullptr,
+           bool after_klein = false) {
     if (!c->has_B) return fail(LGS_ERR_STATE, "lattice points need B (lgs_set_basis B != NULL)");
     BzCall b{Z, zb, ldz, n, V, rb > 0 ? rb : n, rstride, roff, sel};
     static const bool force64 = getenv("LGS_BZ_FP64") && atoi(getenv("LGS_BZ_FP64")) == 1;
@@ -325,7 +342,9 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
     const int8_t* lo = hi + (size_t)c->bd_rows * c->bd_cols;
     HIP_TRY(lgs::launch::bz_i8(Z, zb, ldz, sel, c->kchunk.as<int>(), c->koff.as<int>(), hi, lo,
                                (int)c->bd_cols, (int)c->d, n, V, c->d, b.rb,
-                               b.rstride, b.roff, c->flags.as<unsigned int>(), c->stream));
+                               b.rstride, b.roff, c->flags.as<unsigned int>(),
+                               after_klein && c->hist.Z == Z && Z ? c->H16.as<int16_t>() : nullptr, c->hist.lanes,
+                               c->hist.cols, c->stream));
     c->pending_i8.push_back(b);
     return LGS_OK;
 }
@@ -718,7 +737,7 @@ int lgs_klein(lgs_ctx* c, uint64_t seed, uint64_t first, int64_t n, void* z_out,
         }
         if (v_out) {
             double* V = dev ? v_out + (size_t)off * d : c->V.as<double>();
-            if ((rc = run_bz(c, Zp, zb, a.ldz, m, V))) return rc;
+            if ((rc = run_bz(c, Zp, zb, a.ldz, m, V, 0, 0, 0, nullptr, true))) return rc;
             if ((rc = settle_bz(c))) return rc;
             if (!dev)
                 HIP_TRY(hipMemcpyAsync(v_out + (size_t)off * d, V, (size_t)m * d * 8,
@@ -988,7 +1007,7 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
             if (v_samples) {  // rows (chain, first_keep + k) of the n_chains x n_keep x d output,
                               // read straight from the proposal store through the selections
                 if ((rc = run_bz(c, c->Z.p, zb, ldzb, nq, v_samples, kb, n_keep, first_keep,
-                                 c->sel.as<int64_t>())))
+                                 c->sel.as<int64_t>(), true)))
                     return rc;
             }
             if (z_samples) {

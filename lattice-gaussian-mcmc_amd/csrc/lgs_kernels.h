@@ -186,7 +186,8 @@ hipError_t bz(const void* Z, int zb, int64_t ldz, const int64_t* sel, const doub
 hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const int* kchunk,
                  const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
-                 unsigned int* flags, hipStream_t st);
+                 unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
+                 hipStream_t st);
 // ---- decoding
 // V (row-major n x d) = rows s: sum_c MT[c][r] X[c][s], X coordinate-major fp64 (fp64 MFMA)
 hipError_t gemm_f64(const double* X, int64_t ldx, const double* MT, int d, int64_t n, double* V,

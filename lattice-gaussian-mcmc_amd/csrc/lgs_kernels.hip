@@ -1311,7 +1311,9 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
                                                     const int8_t* __restrict__ Bd0, int dc, int d,
                                                     int64_t n, double* __restrict__ V, int64_t ldv,
                                                     int64_t rb, int64_t rstride, int64_t roff,
-                                                    unsigned int* flags, int tx_count, int64_t ty_count) {
+                                                    unsigned int* flags, int tx_count, int64_t ty_count,
+                                                    const int16_t* __restrict__ h16, int64_t h16_lanes,
+                                                    int64_t hcols) {
     constexpr int TA = LGS_BZ_TA;  // 32-sample MFMA tiles per wave
     constexpr int BM = 64 * TA, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
     constexpr int KPT = KC * BM / 256;  // coefficients per thread per chunk
@@ -1355,7 +1357,25 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
 #endif
     for (int ci = ci0; ci < ci1; ++ci) {
         const int c0 = kchunk[ci] * KC;
-        {  // z chunk -> balanced base-256 digits, [sample][k] byte planes
+        if (KPT == 16 && h16 != nullptr && zs_ < n && zcol < hcols) {
+            // column written by the Klein launch whose int16 history (z + 128,
+            // [coordinate / 16][lane][16]) holds this sample's 16 coefficients in 32
+            // contiguous bytes: the digit planes are byte permutes of them (exact:
+            // that launch checked |z| against the history's range)
+            const v4u_t* hp = (const v4u_t*)(h16 + ((size_t)((c0 + zq * 16) >> 4) * h16_lanes + zcol) * 16);
+            const v4u_t y0 = hp[0], y1 = hp[1];
+            v4i_t w0, w1;
+            w1[0] = (int)__builtin_amdgcn_perm(y0[1], y0[0], 0x07050301u);
+            w1[1] = (int)__builtin_amdgcn_perm(y0[3], y0[2], 0x07050301u);
+            w1[2] = (int)__builtin_amdgcn_perm(y1[1], y1[0], 0x07050301u);
+            w1[3] = (int)__builtin_amdgcn_perm(y1[3], y1[2], 0x07050301u);
+            w0[0] = (int)(__builtin_amdgcn_perm(y0[1], y0[0], 0x06040200u) ^ 0x80808080u);
+            w0[1] = (int)(__builtin_amdgcn_perm(y0[3], y0[2], 0x06040200u) ^ 0x80808080u);
+            w0[2] = (int)(__builtin_amdgcn_perm(y1[1], y1[0], 0x06040200u) ^ 0x80808080u);
+            w0[3] = (int)(__builtin_amdgcn_perm(y1[3], y1[2], 0x06040200u) ^ 0x80808080u);
+            *(v4i_t*)&Zs0[zm * P + zq * 16] = w0;
+            *(v4i_t*)&Zs1[zm * P + zq * 16] = w1;
+        } else {  // z chunk -> balanced base-256 digits, [sample][k] byte planes
             const bool sok = zs_ < n;
             const ZT* zp = Z + (size_t)(c0 + zq * KPT) * ldz + zcol;
 #pragma unroll
@@ -1668,12 +1688,14 @@ hipError_t round_coeffs(const double* W, int64_t ldw, int d, int64_t n, int zb, 
 hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const int* kchunk,
                  const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
-                 unsigned int* flags, hipStream_t st) {
+                 unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
+                 hipStream_t st) {
     if (n <= 0) return hipSuccess;
+    if (d % 16 != 0 || LGS_BZ_TA != 1) h16 = nullptr;  // history blocks must align with the chunks
     const int tx = ((d + 127) / 128 + LGS_BZ_TXPER - 1) / LGS_BZ_TXPER;  // coordinate-tile groups
     const int64_t ty = (n + 64 * LGS_BZ_TA - 1) / (64 * LGS_BZ_TA);
     const dim3 grid((unsigned)(tx * ((ty + 7) / 8) * 8));  // whole rounds of 8 XCDs (extra tiles exit)
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols));
     return hipGetLastError();
 }
 

@@ -152,3 +152,51 @@ def test_imhk_16bit_store_with_wide_carried_states(capi, oracle):
         m = mom.cpu().numpy()
         assert np.array_equal(m[:d], T * zz.sum(0))
         assert np.array_equal(m[d:], T * (zz * zz).sum(0))
+
+
+@pytest.mark.parametrize("wl", [False, True])
+def test_imhk_lattice_points_from_klein_history(capi, oracle, wl):
+    """With the int8-digit far field (NTRU d = 1024, whole 256-proposal blocks) B z
+    reads each proposal's digits from the Klein launch's int16 history and the
+    carried-in states from the store; over two calls with Wang-Ling rejections the
+    kept states mix both sources.  v must equal B z of the kept coefficients."""
+    import torch
+    from lgs_amd.lattices import build_config
+    lat, sigma = build_config("C3_ntru512")
+    B = lat.basis
+    R, cp = oracle.qr_prepare(B)
+    ctx = capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    d, nc, T = B.shape[0], 256, 4
+    dev = "cuda:0"
+    z = torch.zeros((nc, d), dtype=torch.int32, device=dev)
+    lw = torch.zeros(nc, dtype=torch.float64, device=dev)
+    init = torch.zeros(nc, dtype=torch.int32, device=dev)
+    acc = torch.zeros(nc, dtype=torch.int64, device=dev)
+    f = capi.LGS_DEVICE_PTRS | (capi.LGS_WANG_LING if wl else 0)
+    for call in range(2):
+        zs = torch.zeros((nc, T, d), dtype=torch.int32, device=dev)
+        vs = torch.zeros((nc, T, d), dtype=torch.float64, device=dev)
+        ctx.imhk(7, 0, nc, 1 + call * T, T, 1, z, lw, init, acc, z_samples=zs, v_samples=vs, flags=f)
+        zsn = zs.cpu().numpy().reshape(-1, d).astype(np.float64)
+        assert np.array_equal(vs.cpu().numpy().reshape(-1, d), zsn @ B.T)
+    a = acc.cpu().numpy()
+    assert a.sum() == (2 * T * nc if not wl else a.sum())
+    if wl:
+        assert 0 < a.sum() < 2 * T * nc  # some chains kept a carried-in state
+
+
+def test_klein_lattice_points_from_klein_history(capi, oracle):
+    """lgs_klein with lattice points (NTRU d = 1024, 512 samples: int8-digit far
+    field): B z from the launch's history equals B z of the returned coefficients,
+    and the coefficients are the oracle's."""
+    from lgs_amd.lattices import build_config
+    lat, sigma = build_config("C3_ntru512")
+    B = lat.basis
+    R, cp = oracle.qr_prepare(B)
+    ctx = capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    r = ctx.klein_host(4321, 77, 512, want_z=True, want_v=True)
+    assert np.array_equal(r["v"], r["z"].astype(np.float64) @ B.T)
+    o = oracle.klein(R, cp, sigma, 16, seed=4321, first_sample=77)
+    assert np.array_equal(r["z"][:16], o["z"])
