@@ -34,6 +34,17 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector / matrix dense peak (spec)
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def b_alg(d):
     """Algorithmic bytes per Klein sample: fp64 upper triangle of R + int32 z."""
     return 8 * d * (d + 1) // 2 + 4 * d
@@ -227,7 +238,9 @@ def main():
                "kind": "port",
                "sample": f"{n_ch} IMHK chains x {steps_cpu} steps (+1 initial draw), same NTRU "
                          f"d={d} basis, reference-mode weights, {tc:.1f} s wall on {threads} threads",
-               "acceptance": float(accc.sum() / (n_ch * steps_cpu))}
+               "acceptance": float(accc.sum() / (n_ch * steps_cpu)),
+               "per_core": round(props / tc / threads, 2), "host_cpus": os.cpu_count(),
+               "cpu_model": _cpu_model()}
 
     dinfo = ctx.device_info()
     out = {
