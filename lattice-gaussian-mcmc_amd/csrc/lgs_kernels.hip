@@ -809,6 +809,16 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         acc[(15 - s) & 15] = 0.0;  // the next step's logical acc[0]
                     }
                 }
+                // int16 history value (z + 128, clamped to the far field's digit range)
+                auto hist_val = [&](int s) -> int {
+                    if constexpr (sizeof(ZT) == 8)
+                        return (int)(fmin(fmax(zh[s], -32767.0), 32639.0) + 128.0);
+                    else
+                        return min(max(zh[s], -32767), 32639) + 128;
+                };
+                // a whole sub-panel is one 16-coordinate history block ((top + shift) % 16
+                // == 0; position 15 - s holds row top - 1 - s): two 16-byte stores
+                const bool hblock = OZ && rows16 == 16;
 #pragma unroll
                 for (int s = 0; s < 16; ++s) {
                     if (s < rows16) {
@@ -818,12 +828,24 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         else
                             Z[(size_t)i * ldz + p] = (ZT)zh[s];
                         if constexpr (OZ) {  // int16 history (z + 128) for the int8-digit far field
-                            const int ih = i + a.h16_shift;
-                            const double zc = fmin(fmax((double)zh[s], -32767.0), 32639.0);
-                            a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] =
-                                (int16_t)(int)(zc + 128.0);
+                            if (!hblock) {
+                                const int ih = i + a.h16_shift;
+                                a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] = (int16_t)hist_val(s);
+                            }
                             pnz |= zh[s] != 0;
                         }
+                    }
+                }
+                if constexpr (OZ) {
+                    if (hblock) {
+                        v4u_t h[2];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j)
+                            h[j >> 2][j & 3] = ((unsigned int)hist_val(15 - 2 * j) & 0xffffu) |
+                                               ((unsigned int)hist_val(14 - 2 * j) << 16);
+                        v4u_t* hp = (v4u_t*)(a.h16 + ((size_t)((top - 16 + a.h16_shift) >> 4) * a.h16_lanes + p) * 16);
+                        hp[0] = h[0];
+                        hp[1] = h[1];
                     }
                 }
             };
