@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-csv", default=os.environ.get(
-                        "LGS_TRAFFIC_CSV", os.path.join(REPO, "profiles", "r01m_pmc_klein.csv")),
+                        "LGS_TRAFFIC_CSV", os.path.join(REPO, "profiles", "r01n_pmc_klein.csv")),
                     help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE")
     return ap.parse_args()
 

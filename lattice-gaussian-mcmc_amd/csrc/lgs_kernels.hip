@@ -362,7 +362,8 @@ typedef int v4i32_t __attribute__((ext_vector_type(4)));
 typedef double d4_t __attribute__((ext_vector_type(4)));
 
 // Four consecutive coefficients of one coordinate row (one MFMA B fragment
-// column group), loaded non-temporally; raw storage per type, converted to fp64
+// column group), loaded with ordinary (temporal) loads -- measured ~1% faster
+// than non-temporal ones on MI355X; raw storage per type, converted to fp64
 // when the MFMA consumes them (64-bit values are converted exactly).
 template <typename ZT>
 struct ZQuad;
@@ -370,7 +371,7 @@ template <>
 struct ZQuad<int16_t> {
     unsigned long long w;
     __device__ __forceinline__ void load(const int16_t* p) {
-        w = __builtin_nontemporal_load((const unsigned long long*)p);
+        w = *(const unsigned long long*)p;
     }
     __device__ __forceinline__ double get(int g) const { return (double)(short)(w >> (16 * g)); }
 };
@@ -378,7 +379,7 @@ template <>
 struct ZQuad<int32_t> {
     v4i32_t v;
     __device__ __forceinline__ void load(const int32_t* p) {
-        v = __builtin_nontemporal_load((const v4i32_t*)p);
+        v = *(const v4i32_t*)p;
     }
     __device__ __forceinline__ double get(int g) const { return (double)v[g]; }
 };
@@ -387,7 +388,7 @@ struct ZQuad<int64_t> {
     long long v[4];
     __device__ __forceinline__ void load(const int64_t* p) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) v[g] = __builtin_nontemporal_load((const long long*)p + g);
+        for (int g = 0; g < 4; ++g) v[g] = ((const long long*)p)[g];
     }
     __device__ __forceinline__ double get(int g) const { return (double)v[g]; }
 };
@@ -473,11 +474,11 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
         auto hist_load = [&](int ch) {
             const v4u_t* h0 = (const v4u_t*)(hb0 + (size_t)ch * hstep);
             const v4u_t* h1 = (const v4u_t*)(hb1 + (size_t)ch * hstep);
-            w[0][0] = __builtin_nontemporal_load(h0);
-            w[0][1] = __builtin_nontemporal_load(h0 + 1);
+            w[0][0] = *(h0);
+            w[0][1] = *(h0 + 1);
             if constexpr (NG == 2) {
-                w[NG - 1][0] = __builtin_nontemporal_load(h1);
-                w[NG - 1][1] = __builtin_nontemporal_load(h1 + 1);
+                w[NG - 1][0] = *(h1);
+                w[NG - 1][1] = *(h1 + 1);
             } else {
                 (void)h1;
             }
