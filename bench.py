@@ -160,6 +160,7 @@ def main():
     reduce_stats()  # warm torch's lazily loaded kernels and the communicator
     acc.zero_()
     mom.zero_()
+    ctx.resolved(reset=True)
     ctx.timing_enable(True)
     torch.cuda.synchronize()
     if world > 1:
@@ -184,6 +185,7 @@ def main():
     a_ms, a_n = ctx.timing_get(_capi.KERNEL_ACCEPT)
     m_ms, m_n = ctx.timing_get(_capi.KERNEL_MOMENTS)
     acceptance = float(stats[0].item()) / proposals
+    redos = ctx.resolved()
 
     if rank != 0:
         if world > 1:
@@ -263,6 +265,7 @@ def main():
         "imhk_acceptance": round(acceptance, 6),
         "imhk_acceptance_cpu_reference": 1.0,
         "parity_check": f"{parity}/{n_chk} proposals bit-exact vs oracle",
+        "certificate_redos": {"coordinates": redos, "per_proposal": redos / (args.steps * nc * T)},
         "roofline": roofline,
         "gemm": gemm,
         "kernel_ms": {"klein": round(k_ms / max(k_n, 1), 3), "bz": round(g_ms / max(g_n, 1), 3),

@@ -96,6 +96,13 @@ struct lgs_ctx {
     bool has_B = false;
     DevBuf R, RP, RC, BT, coord;  // coord: cp | rii | sig | sig_ref | lterm | irii | ros | isr
     DevBuf CREC, RX;              // 32-row panels: per-coordinate records, coupling blocks
+    DevBuf CERT;                  // per coordinate {Ca, Cb}: decision certificate
+    uint64_t n_resolved = 0;      // sub-panel verifications of uncertified decisions
+    uint64_t n_fallback = 0;      // Klein launches redone with a wider store / fp64 far field
+    // 32-row-panel kernels: the certificate's bound on sum_j |z_j| of a sample (an
+    // estimate from the basis, then twice the largest sum seen; a sample exceeding it
+    // is replayed in the reference's order, so the cap only affects speed)
+    double z1cap = 0.0, z1seen = 0.0;
     DevBuf RD, RDOFF;             // int8-digit far field: R digit fragments, panel offsets
     bool has_rd = false, oz_off = false;  // oz_off: a |z| > 32767 was seen (sticky)
     DevBuf H16, F0;               // int8-digit far field scratch: coefficient history, tile-0 sums
@@ -211,8 +218,22 @@ int finish(lgs_ctx* c) {  // sync, fold timers, report kernel flags
         c->pool.push_back(t.b);
     }
     c->pending.clear();
-    unsigned int f = 0;
-    HIP_TRY(hipMemcpy(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost));
+    unsigned int fw[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpy(fw, c->flags.p, sizeof(fw), hipMemcpyDeviceToHost));
+    const unsigned int f = fw[0];
+    if (fw[1]) {
+        c->n_resolved += fw[1];
+        fw[1] = 0;
+        HIP_TRY(hipMemcpy((unsigned int*)c->flags.p + 1, &fw[1], sizeof(unsigned int), hipMemcpyHostToDevice));
+    }
+    {
+        double z1;
+        memcpy(&z1, fw + 2, sizeof(z1));
+        if (z1 > c->z1seen) {
+            c->z1seen = z1;
+            c->z1cap = 2.0 * z1;
+        }
+    }
     if (f & lgs::kFlagNonFinite)
         return fail(LGS_ERR_NONFINITE, "non-finite conditional mean (reference raises ValueError)");
     if (f & lgs::kFlagOverflow)
@@ -220,6 +241,8 @@ int finish(lgs_ctx* c) {  // sync, fold timers, report kernel flags
     return LGS_OK;
 }
 
+// flags buffer: [0] kernel flag bits, [1] kFlagWordResolved counter, [2..3] the
+// largest sum |z_j| of a Klein launch (fp64 bits, atomicMax)
 int reset_flags(lgs_ctx* c) {
     int rc = c->flags.reserve(16);
     if (rc) return rc;
@@ -250,6 +273,10 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
     a.szc = c->libm_samplez ? nullptr : c->szc.as<double>();
     a.crec = c->CREC.as<double>();
     a.rx = c->RX.as<double>();
+    a.R = c->R.as<double>();
+    a.cert = c->CERT.as<double>();
+    a.z1cap = c->z1cap;
+    a.z1max = (unsigned long long*)c->flags.as<unsigned int>() + 1;
     return a;
 }
 
@@ -310,7 +337,9 @@ int run_klein_store(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int& zb,
         return LGS_OK;
     }
     f &= ~lgs::kFlagOverflow16;
+    c->n_fallback += 1;
     HIP_TRY(hipMemcpy(c->flags.p, &f, sizeof(f), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemsetAsync((unsigned int*)c->flags.p + lgs::kFlagWordResolved, 0, sizeof(unsigned int), c->stream));
     if (zb == 2) {
         c->zint = 4;
         zb = 4;
@@ -500,6 +529,41 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     }
     std::vector<double> szc(dd * lgs::kSzcStride);
     for (size_t i = 0; i < dd; ++i) lgs_host::build_szc(co[2 * dd + i], precision, szc.data() + i * lgs::kSzcStride);
+    // Decision certificate of the blocked kernels (lgs_device.h "certified
+    // decisions"): |mu_fast - mu_ref| <= Ca + Cb * sum_{j>i} |z_j| + 6e-16 |mu|, with
+    // M = max_{j>i} |R_ij|, L1 = sum_{j>i} |R_ij|, u = 2^-53:
+    //  * both sums of R_ij z_j against the exact one: the reference's sequential sum
+    //    gamma_d, the blocked FMA / MFMA sums gamma_{d+40}  -> (2d+80) 1.1 u M Z1;
+    //  * int8-digit far field: R rounded to 2^(E-56) (u M / 2 per unit of z), and the
+    //    recombination of the 8 digit classes, 7 roundings of at most
+    //    sum_j (|R_ij| + 2^E/256)(|z_j| + 512) with 2^E <= 8 M  -> 2 u M Z1 in Cb,
+    //    7.1 u (512 L1 + 16 M d) in Ca;
+    //  * subtraction, reciprocal / division: 5 u |mu| (the kernels' 6e-16 |mu|).
+    std::vector<double> cert(2 * dd, 0.0);
+    {
+        const double u = 0x1p-53, g = (2.0 * (double)d + 80.0) * u;
+        for (size_t i = 0; i < dd; ++i) {
+            double M = 0.0, L1 = 0.0;
+            for (size_t j = i + 1; j < dd; ++j) {
+                const double r = std::fabs(R[i * dd + j]);
+                M = std::max(M, r);
+                L1 += r;
+            }
+            const double ir = 1.0 / std::fabs(R[i * dd + i]);
+            const double ca = 1.01 * 7.1 * u * (512.0 * L1 + 16.0 * M * (double)d) * ir;
+            const double cb = 1.01 * (1.1 * g / (1.0 - g) + 2.0 * u) * M * ir;
+            cert[2 * i] = ca;
+            cert[2 * i + 1] = cb;
+            szc[i * lgs::kSzcStride + lgs::kSzCa] = ca;
+            szc[i * lgs::kSzcStride + lgs::kSzCb] = cb;
+        }
+    }
+    // initial cap on sum_j |z_j| (32-row-panel kernels): window half-widths with room
+    // for the conditional means; replaced by twice the largest sum seen once a launch
+    // has reported it (finish)
+    c->z1seen = 0.0;
+    c->z1cap = 0.0;
+    for (size_t i = 0; i < dd; ++i) c->z1cap += 16.0 * co[2 * dd + i] + 4.0;
     if (getenv("LGS_DEBUG_SZC")) {
         int hist[5] = {0, 0, 0, 0, 0};
         for (size_t i = 0; i < dd; ++i) hist[(int)szc[i * lgs::kSzcStride + 2]]++;
@@ -614,8 +678,9 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     HIP_TRY(hipMemcpy(c->RX.p, rxv.data(), rxv.size() * 8, hipMemcpyHostToDevice));
     if ((rc = c->R.reserve(dd * dd * 8)) || (rc = c->RP.reserve(rp.size() * 8)) ||
         (rc = c->RC.reserve(rcv.size() * 8)) || (rc = c->coord.reserve(co.size() * 8)) ||
-        (rc = c->szc.reserve(szc.size() * 8)))
+        (rc = c->szc.reserve(szc.size() * 8)) || (rc = c->CERT.reserve(cert.size() * 8)))
         return rc;
+    HIP_TRY(hipMemcpy(c->CERT.p, cert.data(), cert.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->szc.p, szc.data(), szc.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->R.p, R, dd * dd * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->RP.p, rp.data(), rp.size() * 8, hipMemcpyHostToDevice));
@@ -1089,6 +1154,16 @@ int lgs_timing_get(lgs_ctx* c, int kernel, double* ms, int64_t* n) {
     if (kernel < 0 || kernel > 5) return fail(LGS_ERR_INVALID, "kernel id 0..5");
     if (ms) *ms = c->t_ms[kernel];
     if (n) *n = c->t_n[kernel];
+    return LGS_OK;
+}
+
+int lgs_counter(lgs_ctx* c, int which, int reset, uint64_t* value) {
+    if (!c) return fail(LGS_ERR_INVALID, "null context");
+    if (which != LGS_COUNTER_RESOLVED && which != LGS_COUNTER_FALLBACK)
+        return fail(LGS_ERR_INVALID, "counter id 0..1");
+    uint64_t& v = which == LGS_COUNTER_RESOLVED ? c->n_resolved : c->n_fallback;
+    if (value) *value = v;
+    if (reset) v = 0;
     return LGS_OK;
 }
 

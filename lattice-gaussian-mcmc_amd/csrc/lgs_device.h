@@ -30,13 +30,20 @@ struct U4 {
     uint32_t x, y, z, w;
 };
 
+template <bool OPAQUE = true>  // false: keys may live in VGPRs (divergent callers)
 __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                             uint32_t k0, uint32_t k1) {
 #ifndef LGS_PHILOX_HOIST
     // opaque to loop-invariant motion: otherwise the 20 round keys of the (kernel-
     // constant) seed are hoisted out of the coordinate loop, spilled to VGPR lanes
-    // and read back with v_readlane + s_nop at every call; recomputing them is 18 SALU adds
-    asm volatile("" : "+s"(k0), "+s"(k1));
+    // and read back with v_readlane + s_nop at every call; recomputing them is 18 SALU
+    // adds.  (readfirstlane: the keys are the same in every lane, and the compiler may
+    // park them in a VGPR across a call)
+    if constexpr (OPAQUE) {
+        k0 = __builtin_amdgcn_readfirstlane(k0);
+        k1 = __builtin_amdgcn_readfirstlane(k1);
+        asm volatile("" : "+s"(k0), "+s"(k1));
+    }
 #endif
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
@@ -78,7 +85,8 @@ __device__ __forceinline__ double accept_uniform(uint64_t seed, uint32_t step, u
 }
 
 // Per-lane coordinate uniform stream: slot k = d-1-i, two slots per Philox call.
-struct CoordStream {
+template <bool OPAQUE = true>
+struct CoordStreamT {
     uint32_t k0, k1, step, chain;
     uint32_t pair;  // cached pair index (0xffffffff = none)
     U4 w;
@@ -99,12 +107,13 @@ struct CoordStream {
 #endif
         const uint32_t p = slot >> 1;
         if (p != pair) {
-            w = philox4x32_10(p, step, chain, kTagCoord, k0, k1);
+            w = philox4x32_10<OPAQUE>(p, step, chain, kTagCoord, k0, k1);
             pair = p;
         }
         return (slot & 1u) ? u53(w.z, w.w) : u53(w.x, w.y);
     }
 };
+using CoordStream = CoordStreamT<true>;
 
 // ------------------------------------------------------------------ SampleZ
 // Support window of _compute_1d_probabilities (klein.py:113-128).
@@ -125,6 +134,58 @@ struct SampleZOut {
     double log_norm;  // log sum_k exp(-(k-mu)^2/(2 sig^2)) over the window (Wang-Ling weight)
 };
 
+// ---------------------------------------------------------- certified decisions
+// The blocked Klein kernels form mu_i in another fp64 order than the reference
+// (blocked FMA / MFMA sums, the int8-digit far field, a reciprocal of R_ii instead
+// of the division of klein.py:191-195).  Every SampleZ function below takes dmu:
+//   dmu < 0   decide at mu (the reference-order kernel, or a redo);
+//   dmu >= 0  a rigorous bound on |mu - mu_ref| (lgs_set_basis: kSzCa / kSzCb):
+//             the decision is returned only when it is the same for EVERY mean
+//             within dmu of mu -- the support window stays put and u stays clear
+//             of every CDF boundary the shift can move -- else kAmbZ / kAmbiguous,
+//             and the kernel recomputes mu in the reference's order for that
+//             coordinate (mu_exact_col) and decides again with dmu < 0.
+// Boundary motion: a mean shift of dmu changes log w_k = -(k-mu)^2/(2 s^2) by
+// (k - mu) dmu / s^2 - dmu^2 / (2 s^2); the k-independent part cancels in every
+// ratio, so the odds C_b / (S - C_b) of a CDF boundary move by a factor of at most
+// E = e^dg, dg = (hi - lo) dmu / s^2 over a window [lo, hi].  Wide windows (s >= 4)
+// use |dP/dmu| = |Cov(k, 1{k<=b})| / s^2 <= sd(k) / (2 s^2) <= 0.6 / s instead.  A
+// 1e-13 S (1e-12 S on the Euler-Maclaurin path) margin covers the rounding of the
+// two evaluations.
+constexpr int64_t kAmbZ = INT64_MIN;
+constexpr double kAmbiguous = __builtin_inf();
+
+// floor(mu - w) and ceil(mu + w) are the same for every mean within dmu of mu
+__device__ __forceinline__ bool ends_stable(double mu, double w, double dmu) {
+    const double tol = 1.01 * dmu + 4.5e-16 * (fabs(mu) + w + 1.0);
+    const double x0 = mu - w, x1 = mu + w;
+    return fabs(x0 - rint(x0)) > tol && fabs(x1 - rint(x1)) > tol;
+}
+// rint(mu) is the same for every mean within dmu of mu (m = mu - rint(mu) is exact)
+__device__ __forceinline__ bool round_stable(double mu, double dmu) {
+    return fabs(mu - rint(mu)) + 1.01 * dmu < 0.5;
+}
+// u S stays on its side of the CDF value Cb (0 <= Cb <= S) when the boundary's odds
+// Cb / (S - Cb) move by a factor of at most E: target (S - Cb) vs E (S - target) Cb
+// (their difference at E = 1 is S (target - Cb))
+__device__ __forceinline__ bool boundary_clear(double target, double Cb, double S, double E) {
+    const double a = target * (S - Cb), b = (S - target) * Cb;
+    return (target > Cb ? a - E * b : b - E * a) > 1e-13 * (S * S);
+}
+// E >= e^dg (fp32 exp2 with the argument and result padded for its rounding);
+// dg beyond the fp32 range gives +inf (nothing is clear)
+__device__ __forceinline__ double odds_factor(double dg) {
+    const float x = (float)(fma(dg, 1.4426950408889634 * 1.000001, 1e-6));
+    return (double)exp2f(x) * 1.000001;
+}
+// support_window (below) is the same for every mean within dmu of mu
+__device__ __forceinline__ bool window_stable(double mu, double sig, int precision, double dmu) {
+    const double rf = (sig < 0.1) ? (double)(precision > 3 ? precision : 3) : (double)precision;
+    if (!ends_stable(mu, rf * sig, dmu)) return false;
+    const double lo = floor(mu - rf * sig), hi = ceil(mu + rf * sig);
+    return !(hi - lo > 1000.0) || round_stable(mu, dmu);
+}
+
 // Decision of klein.py:143-179 for uniform u: the smallest k in the window with
 // cumsum(p)[k] > u * sum(p), p_k proportional to exp(-((k-mu)/sig)^2 / 2).
 // The table is max-shifted (w = 1 at the k nearest mu) instead of normalised by
@@ -133,7 +194,7 @@ struct SampleZOut {
 // Two passes over the window (sum, then cumulative walk); no table storage.
 __device__ __noinline__ SampleZOut sample_z_table(double mu, double sig, int precision,
                                                   bool linear_probs, double u,
-                                                  bool want_log = true) {
+                                                  bool want_log = true, double dmu = -1.0) {
     int64_t lo, hi;
     support_window(mu, sig, precision, lo, hi);
     int64_t ks = (int64_t)rint(mu);
@@ -141,6 +202,12 @@ __device__ __noinline__ SampleZOut sample_z_table(double mu, double sig, int pre
     const double ts = ((double)ks - mu) / sig;
     const double shift = -0.5 * (ts * ts);
     SampleZOut out;
+    const double E = dmu >= 0.0 ? odds_factor((double)(hi - lo) * dmu / (sig * sig)) : 1.0;
+    if (dmu >= 0.0 && (!window_stable(mu, sig, precision, dmu) || (linear_probs && shift < -700.0))) {
+        out.z = kAmbZ;
+        out.log_norm = 0.0;
+        return out;
+    }
     if (linear_probs && exp(shift) == 0.0) {
         // use_log_space=False: every probability underflows -> NaN -> the
         // reference's ValueError fallback round(mean) (klein.py:176-179).
@@ -156,15 +223,22 @@ __device__ __noinline__ SampleZOut sample_z_table(double mu, double sig, int pre
         S += exp(-0.5 * (t * t) - shift);
     }
     const double target = u * S;
-    double C = 0.0;
+    double C = 0.0, Cp = 0.0;
     int64_t z = hi;
     for (int k = 0; k < n; ++k) {
         const double t = ((flo + (double)k) - mu) / sig;
+        Cp = C;
         C += exp(-0.5 * (t * t) - shift);
         if (C > target) {
             z = lo + k;
             break;
         }
+    }
+    if (dmu >= 0.0 && ((z > lo && !boundary_clear(target, Cp, S, E)) ||
+                       (z < hi && !boundary_clear(target, C, S, E)))) {
+        out.z = kAmbZ;
+        out.log_norm = 0.0;
+        return out;
     }
     out.z = z;
     out.log_norm = want_log ? shift + log(S) : 0.0;
@@ -363,7 +437,7 @@ LGS_EM_ATTR double gauss_tab(double kd, double mu, double is, TP etab) {
 template <int NT, typename TP>
 __device__ __forceinline__ SampleZOut sample_z_em_tab(double mu, double sig, int precision,
                                                       bool linear_probs, double u, bool want_log,
-                                                      int64_t lo, int64_t hi, TP etab) {
+                                                      int64_t lo, int64_t hi, TP etab, double dmu) {
     const double is = 1.0 / sig;
     double fL, fU, fk;
     const double PL = em_P_tab<NT>((double)lo, mu, sig, is, etab, fL);
@@ -388,10 +462,17 @@ __device__ __forceinline__ SampleZOut sample_z_em_tab(double mu, double sig, int
         fk = gauss_tab(kd, mu, is, etab);
     }
     const double margin = fmin(Ck - target, kd > flo ? target - (Ck - fk) : target);
-    if (!(margin > 1e-12 * S) || !(Ck > target)) {
+    SampleZOut out;
+    if (dmu >= 0.0) {  // certified: every mean within dmu decides the same
+        if (!(margin > fma(0.6 * dmu, is, 1e-12) * S) || !(Ck > target) ||
+            !window_stable(mu, sig, precision, dmu)) {
+            out.z = kAmbZ;
+            out.log_norm = 0.0;
+            return out;
+        }
+    } else if (!(margin > 1e-12 * S) || !(Ck > target)) {
         return sample_z_table(mu, sig, precision, linear_probs, u, want_log);
     }
-    SampleZOut out;
     out.z = (int64_t)kd;
     out.log_norm = want_log ? log(S) : 0.0;
     return out;
@@ -412,7 +493,7 @@ __device__ __forceinline__ SampleZOut sample_z_em_tab(double mu, double sig, int
 // Same decision rule as sample_z_table: smallest k with cumsum > u * sum.
 __device__ __forceinline__ bool sample_z_small(double mu, double sig, int precision,
                                                bool linear_probs, double u, bool want_log,
-                                               SampleZOut& out) {
+                                               SampleZOut& out, double dmu) {
     int64_t lo, hi;
     support_window(mu, sig, precision, lo, hi);
     if (hi - lo > 3) return false;
@@ -425,6 +506,11 @@ __device__ __forceinline__ bool sample_z_small(double mu, double sig, int precis
         const double t = (((double)lo + (double)k) - mu) * is;
         e[k] = k < n ? -0.5 * (t * t) : -INFINITY;
         emax = fmax(emax, e[k]);
+    }
+    if (dmu >= 0.0 && (!window_stable(mu, sig, precision, dmu) || (linear_probs && emax < -700.0))) {
+        out.z = kAmbZ;
+        out.log_norm = 0.0;
+        return true;
     }
     if (linear_probs && emax < -745.2) {  // every probability underflows: round(mean)
         out.z = (int64_t)rint(mu);
@@ -440,15 +526,26 @@ __device__ __forceinline__ bool sample_z_small(double mu, double sig, int precis
         S += w[k];
     }
     const double target = u * S;
-    double C = 0.0;
+    double C = 0.0, Cp = 0.0, Cz = S;
     int64_t z = hi;
     bool found = false;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        C += w[k];
-        if (!found && k < n && C > target) {
+        const double Cn = C + w[k];
+        if (!found && k < n && Cn > target) {
             z = lo + k;
             found = true;
+            Cp = C;
+            Cz = Cn;
+        }
+        C = Cn;
+    }
+    if (dmu >= 0.0) {
+        const double E = odds_factor((double)(hi - lo) * dmu * (is * is));
+        if ((z > lo && !boundary_clear(target, Cp, S, E)) || (z < hi && !boundary_clear(target, Cz, S, E))) {
+            out.z = kAmbZ;
+            out.log_norm = 0.0;
+            return true;
         }
     }
     out.z = z;
@@ -458,17 +555,18 @@ __device__ __forceinline__ bool sample_z_small(double mu, double sig, int precis
 
 // etab == nullptr selects the libm Euler-Maclaurin path (ocml erf/exp/erfinv).
 LGS_SAMPLEZ_ATTR SampleZOut sample_z(double mu, double sig, int precision, bool linear_probs,
-                                     double u, bool want_log, const double* __restrict__ etab) {
+                                     double u, bool want_log, const double* __restrict__ etab,
+                                     double dmu = -1.0) {
     if (sig < kEMMin) {
         SampleZOut o;
-        if (sample_z_small(mu, sig, precision, linear_probs, u, want_log, o)) return o;
-        return sample_z_table(mu, sig, precision, linear_probs, u, want_log);
+        if (sample_z_small(mu, sig, precision, linear_probs, u, want_log, o, dmu)) return o;
+        return sample_z_table(mu, sig, precision, linear_probs, u, want_log, dmu);
     }
     int64_t lo, hi;
     support_window(mu, sig, precision, lo, hi);
     if (etab) {
-        return sig < 50.0 ? sample_z_em_tab<6>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab)
-                          : sample_z_em_tab<3>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab);
+        return sig < 50.0 ? sample_z_em_tab<6>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab, dmu)
+                          : sample_z_em_tab<3>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab, dmu);
     }
     const double is = 1.0 / sig;
     double fL, fU, fk;
@@ -497,10 +595,17 @@ LGS_SAMPLEZ_ATTR SampleZOut sample_z(double mu, double sig, int precision, bool 
         fk = exp(-0.5 * (t * t));
     }
     const double margin = fmin(Ck - target, kd > flo ? target - (Ck - fk) : target);
-    if (!(margin > 1e-12 * S) || !(Ck > target)) {
+    SampleZOut out;
+    if (dmu >= 0.0) {
+        if (!(margin > fma(0.6 * dmu, is, 1e-12) * S) || !(Ck > target) ||
+            !window_stable(mu, sig, precision, dmu)) {
+            out.z = kAmbZ;
+            out.log_norm = 0.0;
+            return out;
+        }
+    } else if (!(margin > 1e-12 * S) || !(Ck > target)) {
         return sample_z_table(mu, sig, precision, linear_probs, u, want_log);
     }
-    SampleZOut out;
     out.z = (int64_t)kd;
     out.log_norm = want_log ? log(S) : 0.0;
     return out;
@@ -521,10 +626,10 @@ __device__ __forceinline__ double em_C_rel(double kd, double m, double sig, doub
     return em_P_tab<NT>(kd, m, sig, is, etab, fk) + 0.5 * fk - base;
 }
 
-template <int NT, typename TP, typename QP>
+template <int NT, bool CERT, typename TP, typename QP>
 __device__ __forceinline__ double sample_z_wide(double mu, double u, QP q,
                                                 int kind, int precision, bool linear_probs,
-                                                bool want_log, TP etab, double& log_norm) {
+                                                bool want_log, TP etab, double& log_norm, double dmu) {
     const double sig = q[0], is = q[1];
     const double c = rint(mu);
     const double m = mu - c;
@@ -565,9 +670,21 @@ __device__ __forceinline__ double sample_z_wide(double mu, double u, QP q,
         fk = gauss_tab(kd, m, is, etab);
     }
     const double margin = fmin(Ck - target, kd > a ? target - (Ck - fk) : target);
-    // too close to call in fp64 (margin below 1e-12 S): sample_z_coord finishes
-    // it with the exact table walk
-    if (!(margin > 1e-12 * S) || !(Ck > target)) return __builtin_nan("");
+    if constexpr (CERT) {
+        // certificate: clear of the boundaries by the 0.6 dmu / s they can move;
+        // a capped window is c +- 500 for every mean within dmu; the closed
+        // window's ends carry < 1e-18 S (tails beyond +-9 s).  Not covered: the
+        // decision as a guess, flagged by log_norm = NaN
+        if (!(Ck > target)) return __builtin_nan("");
+        if (!(margin > fma(0.6 * dmu, is, 1e-12) * S) || (kind == kSzCapped && !(fabs(m) + 1.01 * dmu < 0.5))) {
+            log_norm = __builtin_nan("");
+            return c + kd;
+        }
+    } else if (!(margin > 1e-12 * S) || !(Ck > target)) {
+        // too close to call in fp64 (margin below 1e-12 S): sample_z_coord
+        // finishes it with the exact table walk
+        return __builtin_nan("");
+    }
     log_norm = want_log ? log(S) : 0.0;
     return c + kd;
 }
@@ -578,11 +695,11 @@ __device__ __forceinline__ double sample_z_wide(double mu, double u, QP q,
 template <typename TP>
 __device__ __noinline__ SampleZOut sample_z_generic(double mu, double sig, int precision,
                                                     bool linear_probs, double u, bool want_log,
-                                                    TP etab) {
+                                                    TP etab, double dmu) {
     int64_t lo, hi;
     support_window(mu, sig, precision, lo, hi);
-    return sig < 50.0 ? sample_z_em_tab<6>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab)
-                      : sample_z_em_tab<3>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab);
+    return sig < 50.0 ? sample_z_em_tab<6>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab, dmu)
+                      : sample_z_em_tab<3>(mu, sig, precision, linear_probs, u, want_log, lo, hi, etab, dmu);
 }
 
 // A wave-uniform pointer passed to a non-inlined function arrives in VGPRs;
@@ -604,6 +721,7 @@ __device__ __forceinline__ cdptr uniformize(cdptr p) {
     return (cdptr)(((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ lds_cdptr uniformize(lds_cdptr p) { return p; }
+__device__ __forceinline__ gdptr uniformize(gdptr p) { return p; }  // (divergent callers)
 
 // The per-coordinate decision proper is a leaf function: it makes no calls, so
 // it needs no frame (a non-leaf callee saves its return address through a
@@ -611,10 +729,10 @@ __device__ __forceinline__ lds_cdptr uniformize(lds_cdptr p) { return p; }
 // handle -- small-kind windows of more than 4 points, the generic kind and wide
 // decisions within 1e-12 S of a boundary -- return NaN, and sample_z_coord
 // below finishes them out of line.
-template <typename TP, typename QP>
+template <bool CERT, typename TP, typename QP>
 __device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qin, int precision,
                                                       bool linear_probs, bool want_log, TP etab,
-                                                      double& log_norm) {
+                                                      double& log_norm, double dmu) {
     const QP q = uniformize(qin);  // all lanes are on the same coordinate
     const int kind = (int)q[2];
     const double sig = q[0];
@@ -623,15 +741,24 @@ __device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qi
         const double hi = ceil(mu + q[6]);
         if (hi - lo > 3.0) return __builtin_nan("");
         const double is = q[1];
+        constexpr bool cert = CERT;
+        // window ends: checked when the points they can add or drop may carry more
+        // than 2^-60 of the mass (q[7], host); otherwise such a point only matters for
+        // u < 2^-60, i.e. u = 0.  Not covered: the decision as a guess, log_norm = NaN
+        const bool doubt = cert && (q[7] != 0.0 ? !ends_stable(mu, q[6], dmu) : u == 0.0);
         if (hi - lo == 1.0) {
             // two points whose weights differ by more than e^745.2: the smaller
             // one is exactly 0 in fp64 (as in the general loop below), so the
-            // decision is the heavier point for every u
+            // decision is the heavier point for every u -- certified when the gap
+            // (moving at 1/s^2 per unit of mean) stays above 745.2 within dmu
             const double t0 = (lo - mu) * is, t1 = (hi - mu) * is;
             const double e0 = -0.5 * (t0 * t0), e1 = -0.5 * (t1 * t1);
             const double em = fmax(e0, e1);
-            if (fmin(e0, e1) - em < -745.2 && !(linear_probs && em < -745.2)) {
-                log_norm = want_log ? em : 0.0;
+            const double gap = em - fmin(e0, e1);
+            if (gap > 745.2 && !(linear_probs && em < -745.2)) {
+                log_norm = (doubt || (cert && !(gap - 745.2 > 1.01 * dmu * (is * is) + 1e-12 * gap)))
+                               ? __builtin_nan("")
+                               : (want_log ? em : 0.0);
                 return e0 > e1 ? lo : hi;
             }
         }
@@ -644,7 +771,7 @@ __device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qi
             emax = fmax(emax, e[k]);
         }
         if (linear_probs && emax < -745.2) {
-            log_norm = -INFINITY;
+            log_norm = cert ? __builtin_nan("") : -INFINITY;
             return rint(mu);
         }
         double w[4];
@@ -656,23 +783,33 @@ __device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qi
             Ssum += w[k];
         }
         const double target = u * Ssum;
-        double C = 0.0, z = hi;
+        double C = 0.0, z = hi, Cp = 0.0, Cz = Ssum;
         bool found = false;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            C += w[k];
-            if (!found && lo + (double)k <= hi && C > target) {
+            const double Cn = C + w[k];
+            if (!found && lo + (double)k <= hi && Cn > target) {
                 z = lo + (double)k;
                 found = true;
+                Cp = C;
+                Cz = Cn;
             }
+            C = Cn;
         }
         log_norm = want_log ? emax + log(Ssum) : 0.0;
+        if (cert) {
+            // boundary odds move by at most e^{(hi - lo) dmu / s^2}
+            const double E = odds_factor((hi - lo) * dmu * (is * is));
+            if (doubt || (linear_probs && emax < -700.0) || (z > lo && !boundary_clear(target, Cp, Ssum, E)) ||
+                (z < hi && !boundary_clear(target, Cz, Ssum, E)))
+                log_norm = __builtin_nan("");
+        }
         return z;
     }
     if (kind == kSzGeneric) return __builtin_nan("");
     return sig < 50.0
-               ? sample_z_wide<6>(mu, u, q, kind, precision, linear_probs, want_log, etab, log_norm)
-               : sample_z_wide<3>(mu, u, q, kind, precision, linear_probs, want_log, etab, log_norm);
+               ? sample_z_wide<6, CERT>(mu, u, q, kind, precision, linear_probs, want_log, etab, log_norm, dmu)
+               : sample_z_wide<3, CERT>(mu, u, q, kind, precision, linear_probs, want_log, etab, log_norm, dmu);
 }
 
 // Both results come back in registers (a reference parameter of a call lives in
@@ -680,38 +817,81 @@ __device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qi
 struct SzPair {
     double z, ln;
 };
-template <typename TP, typename QP>
+template <bool CERT, typename TP, typename QP>
 LGS_SAMPLEZ_ATTR SzPair sample_z_coord_leaf(double mu, double u, QP q, int precision,
-                                            bool linear_probs, bool want_log, TP etab) {
+                                            bool linear_probs, bool want_log, TP etab, double dmu) {
     SzPair r;
     r.ln = 0.0;
-    r.z = sample_z_coord_body(mu, u, q, precision, linear_probs, want_log, etab, r.ln);
+    r.z = sample_z_coord_body<CERT>(mu, u, q, precision, linear_probs, want_log, etab, r.ln, dmu);
     return r;
 }
 
 template <typename TP>
 __device__ __noinline__ double sample_z_coord_fallback(double mu, double u, double sig, int kind,
                                                        int precision, bool linear_probs,
-                                                       bool want_log, TP etab, double& log_norm) {
+                                                       bool want_log, TP etab, double& log_norm,
+                                                       double dmu) {
     const SampleZOut o = kind == kSzGeneric
-                             ? sample_z_generic(mu, sig, precision, linear_probs, u, want_log, etab)
-                             : sample_z_table(mu, sig, precision, linear_probs, u, want_log);
+                             ? sample_z_generic(mu, sig, precision, linear_probs, u, want_log, etab, dmu)
+                             : sample_z_table(mu, sig, precision, linear_probs, u, want_log, dmu);
     log_norm = o.log_norm;
-    return (double)o.z;
+    return o.z == kAmbZ ? kAmbiguous : (double)o.z;
 }
 
 // SampleZ for one coordinate from its precomputed constants (kinds in lgs_kernels.h).
+// dmu >= 0: certified decision (see "certified decisions" above; kAmbiguous when
+// not covered); dmu < 0: plain decision at mu.
 template <typename TP, typename QP>
 __device__ __forceinline__ double sample_z_coord(double mu, double u, QP q, int precision,
                                                  bool linear_probs, bool want_log, TP etab,
-                                                 double& log_norm) {
-    const SzPair r = sample_z_coord_leaf(mu, u, q, precision, linear_probs, want_log, etab);
+                                                 double& log_norm, double dmu) {
+    const SzPair r = dmu >= 0.0
+                         ? sample_z_coord_leaf<true>(mu, u, q, precision, linear_probs, want_log, etab, dmu)
+                         : sample_z_coord_leaf<false>(mu, u, q, precision, linear_probs, want_log, etab, dmu);
     double z = r.z;
     log_norm = r.ln;
+    if (dmu >= 0.0 && !__builtin_isnan(z) && __builtin_isnan(r.ln)) return kAmbiguous;
     if (__builtin_isnan(z))
         z = sample_z_coord_fallback(mu, u, q[0], (int)q[2], precision, linear_probs, want_log, etab,
-                                    log_norm);
+                                    log_norm, dmu);
     return z;
+}
+// The same with the certificate fixed at compile time (hot loops: one call target).
+// The same with the certificate fixed at compile time (hot loops: one call target);
+// CERT: always returns a decision (a guess when not covered: amb = true, log_norm = 0).
+template <bool CERT, typename TP, typename QP>
+__device__ __forceinline__ double sample_z_coord_t(double mu, double u, QP q, int precision,
+                                                   bool linear_probs, bool want_log, TP etab,
+                                                   double& log_norm, double dmu, bool& amb) {
+    const SzPair r = sample_z_coord_leaf<CERT>(mu, u, q, precision, linear_probs, want_log, etab, dmu);
+    double z = r.z;
+    log_norm = r.ln;
+    amb = false;
+    if (__builtin_isnan(z)) {
+        z = sample_z_coord_fallback(mu, u, q[0], (int)q[2], precision, linear_probs, want_log, etab,
+                                    log_norm, CERT ? dmu : -1.0);
+        if (CERT && z == kAmbiguous) {
+            z = rint(mu);
+            amb = true;
+        }
+    } else if (CERT && __builtin_isnan(r.ln)) {
+        amb = true;
+    }
+    if (amb) log_norm = 0.0;
+    return z;
+}
+
+// Conditional mean of coordinate i in the reference's order (klein.py:191-195:
+// j ascending, separate multiply and add -- the file is built with
+// -ffp-contract=off), from the sample's own stored coefficients z_j, j > i.
+// Used for the rare decisions the certificate does not cover.
+template <typename ZT>
+__device__ __noinline__ double mu_exact_col(const double* __restrict__ R, const ZT* __restrict__ Zp,
+                                            size_t ldz, int i, int d, double cp, double rii) {
+    const double* __restrict__ Ri = R + (size_t)i * d;
+    double cs = 0.0;
+    for (int j = i + 1; j < d; ++j) cs = cs + Ri[j] * (double)Zp[(size_t)j * ldz];
+    return (cp - cs) / rii;
 }
 
 }  // namespace lgs

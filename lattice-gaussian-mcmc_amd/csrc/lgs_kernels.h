@@ -10,6 +10,9 @@ constexpr unsigned int kFlagNonFinite = 1u;  // a conditional mean was NaN/inf
 constexpr unsigned int kFlagOverflow = 2u;   // |z| >= 2^31 with an int32 store
 constexpr unsigned int kFlagI8Range = 4u;    // |z| > 32639: int8-digit B z must be redone in fp64
 constexpr unsigned int kFlagOverflow16 = 8u; // |z| > 32767 in a 16-bit internal store
+// flags[1] of a launch: coordinates whose decision at the blocked-order mean could
+// not be certified and was redone at the reference-order mean (lgs_device.h)
+constexpr int kFlagWordResolved = 1;
 
 constexpr int kErfTabLast = 512;
 constexpr int kCoefStride = 18;  // doubles per grid point of the coefficient table (lgs_device.h CoefTab)  // SampleZ erf/exp table: y_j = j/64, j = 0..kErfTabLast (y <= 8)
@@ -21,10 +24,16 @@ constexpr int kCoefStride = 18;  // doubles per grid point of the coefficient ta
 //   [7] S, [8] base (kind kSzClosed)
 //   [kSzS..kSzS+kSzDeg] / [kSzB..kSzB+kSzDeg]: monomial coefficients in
 //   m = mu - rint(mu) of S(m) / base(m) (kind kSzCapped)
+//   [kSzCa], [kSzCb]: decision certificate of the blocked kernels (lgs_device.h
+//   certified decisions): |mu_fast - mu_ref| <= Ca + Cb * sum_{j>i} |z_j| + 6e-16 |mu|
+//   [7] of the small kind: 1 when points entering / leaving the window at its ends
+//   can carry more than 2^-60 of the mass (the certificate then checks the ends)
 constexpr int kSzDeg = 5;  // degree 4 already reaches the fp64 floor for sigma in [50, 1e6]
 constexpr int kSzS = 9;
 constexpr int kSzB = kSzS + kSzDeg + 1;
-constexpr int kSzUsed = kSzB + kSzDeg + 1;  // 21
+constexpr int kSzCa = kSzB + kSzDeg + 1;  // 21
+constexpr int kSzCb = kSzCa + 1;
+constexpr int kSzUsed = kSzCb + 1;  // 23
 constexpr int kSzcStride = 24;
 // Klein-path record per coordinate (kRecStride doubles): the SampleZ constants
 // [0, kSzUsed), then c', 1/R_ii, R_ii/sigma, 1/sigma_i^ref, lterm, and the 15
@@ -35,7 +44,7 @@ constexpr int kRecCp = kSzUsed, kRecIrii = kSzUsed + 1, kRecRos = kSzUsed + 2,
 // int8-digit far field (klein_mfma_kernel OZ): row scale 2^E_i of the
 // coordinate's row over its panel's far columns
 constexpr int kRecScale = kRecRs + 15;
-constexpr int kRecStride = kRecRs + 18;  // 44: 352 bytes, 16-byte multiple
+constexpr int kRecStride = kRecRs + 18;  // 46: 368 bytes, 16-byte multiple
 // int8-digit far field layout: per 32-row panel pk >= 1 (K = 32 pk far columns,
 // ceil(K/64) chunks of 64): [chunk][row tile t][digit a][lane][16 bytes]
 constexpr int kOzDigits = 7;
@@ -72,7 +81,10 @@ struct KleinArgs {
     const double* irii;
     const double* ros;
     const double* isr;
+    const double* R;     // row-major R (reference-order means of uncertified decisions)
     double sigma;
+    double z1cap;        // 32-row panels: certificate bound on sum_j |z_j| (verified per sub-panel)
+    unsigned long long* z1max;  // 32-row panels: atomicMax of the samples' sum |z_j| (fp64 bits)
     uint64_t seed;
     uint64_t base;
     uint32_t chain0;
@@ -85,6 +97,7 @@ struct KleinArgs {
     const double* etab;  // SampleZ erf/exp table (nullptr: ocml libm path)
     const double* etab2; // its Taylor-coefficient form (lgs_device.h CoefTab)
     const double* szc;   // per-coordinate SampleZ constants (nullptr: generic sample_z)
+    const double* cert;  // per coordinate {Ca, Cb} of the decision certificate (kSzCa / kSzCb)
     const double* crec;  // per-coordinate records (kRecStride doubles, layout above)
     // int8-digit far field (nullptr rd: fp64 MFMA far field)
     const int8_t* rd;        // R digit fragments, all panels

@@ -26,6 +26,8 @@
 
 namespace lgs {
 
+typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ void lane_counter(const KleinArgs& a, int64_t p, uint32_t& chain,
                                              uint32_t& step) {
     if (a.counter_mode == 0) {
@@ -38,11 +40,32 @@ __device__ __forceinline__ void lane_counter(const KleinArgs& a, int64_t p, uint
     }
 }
 
+// Reference-mode importance weight term of one coordinate (imhk.py:102-124):
+// log_gaussian_weight(Bz) - compute_log_density(Bz), with ||Bz - c||^2 =
+// sum_i (R_ii (z_i - mu_i))^2.
+__device__ __forceinline__ double ref_weight(double zi, double mu, double ros, double isr, double lterm) {
+    const double res = zi - mu;
+    const double ta = res * ros;
+    const double tq = res * isr;
+    return (-0.5 * (ta * ta)) - (-0.5 * (tq * tq) - lterm);
+}
+
+// Certificate bound dmu >= |mu - mu_ref| of coordinate i (lgs_device.h "certified
+// decisions"; constants from lgs_set_basis), z1 = sum_{j>i} |z_j| of the sample.
+__device__ __forceinline__ double cert_dmu(double ca, double cb, double z1, double mu) {
+#ifdef LGS_DIAG_NO_CERT  // diagnostic builds only: cost probe of the certificate (NOT bit-exact)
+    return -1.0;
+#endif
+    return fma(cb, z1, ca) + 6e-16 * fabs(mu);
+}
+
 // One coordinate's decision + weight bookkeeping, shared by both samplers.
+// dmu >= 0: certified decision (kAmbiguous when the reference-order mean could
+// decide otherwise; lw is then untouched); dmu < 0: decide at mu.
 template <bool WL, typename TP>
 __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double mu,
                                                CoordStream& rs, double& lw, unsigned int& flags,
-                                               TP etab) {
+                                               TP etab, double dmu) {
     double zi;
     if (!isfinite(mu)) {
         flags |= kFlagNonFinite;
@@ -61,34 +84,31 @@ __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double
 #endif
     if (s == 0.0) {  // sigma_i < 1e-10: round, no draw (klein.py:201-204)
         zi = rint(mu);
+        if (dmu >= 0.0 && !round_stable(mu, dmu)) return kAmbiguous;
     } else if (a.szc) {
         double ln;
         zi = sample_z_coord(mu, rs.u((uint32_t)(a.d - 1 - i)), cst(a.szc) + (size_t)i * kSzcStride,
-                            a.precision, a.linear_probs != 0, WL, etab, ln);
+                            a.precision, a.linear_probs != 0, WL, etab, ln, dmu);
+        if (zi == kAmbiguous) return kAmbiguous;
         if (WL) lw += ln;
     } else {
         SampleZOut o = sample_z(mu, s, a.precision, a.linear_probs != 0,
-                                rs.u((uint32_t)(a.d - 1 - i)), WL, a.etab);
+                                rs.u((uint32_t)(a.d - 1 - i)), WL, a.etab, dmu);
+        if (o.z == kAmbZ) return kAmbiguous;
         zi = (double)o.z;
         if (WL) lw += o.log_norm;
     }
-    if (!WL) {
-        // Reference-mode importance weight (imhk.py:102-124): log_gaussian_weight(Bz)
-        // - compute_log_density(Bz), with ||Bz - c||^2 = sum_i (R_ii (z_i - mu_i))^2.
-        const double res = zi - mu;
-        const double ta = res * cst(a.ros)[i];
-        const double tq = res * cst(a.isr)[i];
-        lw += (-0.5 * (ta * ta)) - (-0.5 * (tq * tq) - cst(a.lterm)[i]);
-    }
+    if (!WL) lw += ref_weight(zi, mu, cst(a.ros)[i], cst(a.isr)[i], cst(a.lterm)[i]);
     return zi;
 }
 
 // decide_coord with the coordinate's record rec staged in LDS (klein_mfma_kernel, 32-row panels).
-template <bool WL, typename TP>
+template <bool WL, bool CERT, typename TP>
 __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, double mu,
                                                    lds_cdptr rec, CoordStream& rs, double& lw,
-                                                   unsigned int& flags, TP etab) {
+                                                   unsigned int& flags, TP etab, double dmu, bool& amb) {
     double zi = 0.0;
+    amb = false;
     if (!isfinite(mu)) {
         flags |= kFlagNonFinite;
         return 0.0;
@@ -104,45 +124,28 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         zi = rint(mu + rs.u((uint32_t)(a.d - 1 - i)) * 1e-300);
     } else
 #endif
+    // CERT: a decision not covered by the certificate is returned as a guess with
+    // amb set and no weight term (the sub-panel's verification adds it); selects
+    // instead of early returns keep the weight update branch-free (measured 13 vs
+    // 44 spilled VGPRs)
     if (s == 0.0) {
         zi = rint(mu);
+        amb = CERT && !round_stable(mu, dmu);
     } else if (!a.szc) {  // LGS_SAMPLEZ_LIBM: generic path
         SampleZOut o = sample_z(mu, s, a.precision, a.linear_probs != 0,
-                                rs.u((uint32_t)(a.d - 1 - i)), WL, a.etab);
-        zi = (double)o.z;
-        if (WL) lw += o.log_norm;
+                                rs.u((uint32_t)(a.d - 1 - i)), WL, a.etab, CERT ? dmu : -1.0);
+        amb = CERT && o.z == kAmbZ;
+        zi = amb ? rint(mu) : (double)o.z;
+        if (WL) lw += amb ? 0.0 : o.log_norm;
     } else {
-        // inline two-point decision of the small kind (see sample_z_coord): when one
-        // weight is exactly 0 the decision does not depend on u, so no draw is made
-        // (draws are counter-addressed: skipping one shifts nothing)
-        bool done = false;
-#ifdef LGS_INLINE_SMALL  // measured slower (register pressure in the near field)
-        if ((int)rec[2] == kSzSmall) {
-            const double lo = floor(mu - rec[6]), hi = ceil(mu + rec[6]);
-            if (hi - lo == 1.0) {
-                const double t0 = (lo - mu) * rec[1], t1 = (hi - mu) * rec[1];
-                const double e0 = -0.5 * (t0 * t0), e1 = -0.5 * (t1 * t1);
-                const double em = fmax(e0, e1);
-                if (fmin(e0, e1) - em < -745.2 && !(a.linear_probs && em < -745.2)) {
-                    zi = e0 > e1 ? lo : hi;
-                    if (WL) lw += em;
-                    done = true;
-                }
-            }
-        }
-#endif
-        if (!done) {
-            double ln;
-            zi = sample_z_coord(mu, rs.u((uint32_t)(a.d - 1 - i)), rec, a.precision,
-                                a.linear_probs != 0, WL, etab, ln);
-            if (WL) lw += ln;
-        }
+        double ln;
+        zi = sample_z_coord_t<CERT>(mu, rs.u((uint32_t)(a.d - 1 - i)), rec, a.precision,
+                                    a.linear_probs != 0, WL, etab, ln, dmu, amb);
+        if (WL) lw += ln;
     }
     if (!WL) {
-        const double res = zi - mu;
-        const double ta = res * rec[kRecRos];
-        const double tq = res * rec[kRecIsr];
-        lw += (-0.5 * (ta * ta)) - (-0.5 * (tq * tq) - rec[kRecLterm]);
+        const double t = ref_weight(zi, mu, rec[kRecRos], rec[kRecIsr], rec[kRecLterm]);
+        lw += amb ? 0.0 : t;
     }
     return zi;
 }
@@ -168,6 +171,250 @@ __device__ __forceinline__ lds_cdptr stage_etab(double* tab_lds, const double* _
     return (lds_cdptr)tab_lds;
 }
 
+// A decision the certificate does not cover (rare; lanes diverge): the
+// coordinate's mean in the reference's order from the sample's stored z_j (j > i,
+// Zp = &Z[0][p]), then the plain decision at that mean with the same uniform.
+// Out of line, with every input as a plain value.  Counted in *cnt.
+struct Resolved {
+    double z, ln, mu;
+};
+template <typename ZT>
+__device__ __noinline__ Resolved resolve_decision(const double* __restrict__ R, const ZT* __restrict__ Zp,
+                                                  size_t ldz, int i, int d, double cp, double rii,
+                                                  const double* __restrict__ q, double s, double u,
+                                                  int precision, bool linear, bool want_log,
+                                                  const double* __restrict__ etab, unsigned int* cnt) {
+    Resolved r;
+    r.mu = mu_exact_col(R, Zp, ldz, i, d, cp, rii);
+    r.ln = 0.0;
+    r.z = 0.0;
+    atomicAdd(cnt, 1u);
+    if (!isfinite(r.mu)) return r;
+    if (s == 0.0) {
+        r.z = rint(r.mu);
+    } else if (q) {
+        r.z = sample_z_coord(r.mu, u, (gdptr)q, precision, linear, want_log, (gdptr)etab, r.ln, -1.0);
+    } else {
+        const SampleZOut o = sample_z(r.mu, s, precision, linear, u, want_log, etab);
+        r.z = (double)o.z;
+        r.ln = o.log_norm;
+    }
+    return r;
+}
+
+template <bool WL, typename ZT>
+__device__ __forceinline__ double resolve_coord(const KleinArgs& a, int i, const ZT* Zp, size_t ldz,
+                                                CoordStream& rs, double& lw, unsigned int& flags) {
+    const size_t iq = (size_t)i * kSzcStride;
+    const Resolved r = resolve_decision(a.R, Zp, ldz, i, a.d, cst(a.cp)[i], cst(a.rii)[i],
+                                        a.szc ? a.szc + iq : nullptr,
+                                        a.szc ? cst(a.szc)[iq] : cst(a.sig)[i], rs.u((uint32_t)(a.d - 1 - i)),
+                                        a.precision, a.linear_probs != 0, WL, a.etab,
+                                        a.flags + kFlagWordResolved);
+    if (!isfinite(r.mu)) {
+        flags |= kFlagNonFinite;
+        return 0.0;
+    }
+    lw += WL ? r.ln : ref_weight(r.z, r.mu, cst(a.ros)[i], cst(a.isr)[i], cst(a.lterm)[i]);
+    return r.z;
+}
+
+// mu_exact_col from the int16 history of the int8-digit far field (z + 128, exact
+// for |z| <= 32639, which the OZ kernel guarantees): the 16 coefficients of a
+// 16-coordinate block are 32 contiguous bytes of the lane, so the column costs d/16
+// loads instead of d strided ones (whose latency would dominate a replay).
+__device__ __noinline__ double mu_exact_hist(const double* __restrict__ R, const int16_t* __restrict__ hl,
+                                             int64_t lanes, int shift, int i, int d, double cp, double rii) {
+    const double* __restrict__ Ri = R + (size_t)i * d;
+    const size_t bstride = (size_t)lanes * 16;  // int16 elements between 16-coordinate blocks
+    double cs = 0.0;
+    const int b0 = (i + 1 + shift) >> 4, bl = (d - 1 + shift) >> 4;
+    v4u_t w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0};
+    if (b0 <= bl) {
+        w0 = ((const v4u_t*)(hl + (size_t)b0 * bstride))[0];
+        w1 = ((const v4u_t*)(hl + (size_t)b0 * bstride))[1];
+    }
+    for (int b = b0; b <= bl; ++b) {
+        v4u_t n0 = w0, n1 = w1;
+        if (b < bl) {  // next block in flight while this one is summed
+            n0 = ((const v4u_t*)(hl + (size_t)(b + 1) * bstride))[0];
+            n1 = ((const v4u_t*)(hl + (size_t)(b + 1) * bstride))[1];
+        }
+        const int j0 = b * 16 - shift;  // coordinate at position 0 of the block
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const unsigned int wd = k < 8 ? w0[(k >> 1) & 3] : w1[(k >> 1) & 3];
+            const int h = (int)(int16_t)(uint16_t)((k & 1) ? (wd >> 16) : (wd & 0xffffu));  // signed
+            const int j = j0 + k;
+            if (j > i && j < d) cs = cs + Ri[j] * (double)(h - 128);
+        }
+        w0 = n0;
+        w1 = n1;
+    }
+    return (cp - cs) / rii;
+}
+
+// Reference-order conditional mean of coordinate i of ONE sample (lane L of the
+// calling wave), computed by the whole wave: lane k loads R_ij and z_j of
+// j = j0 + k and forms the product (exactly the reference's rounded product), and
+// the products are then added one at a time in ascending j (klein.py:191-195) --
+// the serial part is 2 readlanes + 1 add per term instead of a latency-bound walk
+// of one lane over R and its coefficients.  z_j: the int16 history (OZ; hL = the
+// sample's base, exact for |z| <= 32639) or the coefficient store (zL = &Z[0][p]).
+// All arguments wave-uniform; call from uniform control flow.
+template <typename ZT>
+__device__ __forceinline__ double mu_exact_wave(const double* __restrict__ R, const int16_t* __restrict__ hL,
+                                                int64_t lanes, int shift, const ZT* __restrict__ zL,
+                                                size_t ldz, int i, int d, double cp, double rii) {
+    const int lane = threadIdx.x & 63;
+    const double* __restrict__ Ri = R + (size_t)i * d;
+    auto load = [&](int j0, double& r, double& z) {
+        const int j = j0 + lane;
+        r = 0.0;
+        z = 0.0;
+        if (j < d) {
+            r = Ri[j];
+            if (hL) {
+                const int ih = j + shift;
+                z = (double)((int)hL[(size_t)(ih >> 4) * lanes * 16 + (ih & 15)] - 128);
+            } else {
+                z = (double)zL[(size_t)j * ldz];
+            }
+        }
+    };
+    double cs = 0.0, r, z;
+    load(i + 1, r, z);
+    for (int j0 = i + 1; j0 < d; j0 += 64) {
+        const double pr = r * z;  // this lane's term (unfused: -ffp-contract=off)
+        if (j0 + 64 < d) load(j0 + 64, r, z);  // next chunk in flight
+        const int m = min(64, d - j0);
+        const long long bits = __double_as_longlong(pr);
+        const int lo = (int)bits, hi = (int)(bits >> 32);
+        for (int k = 0; k < m; ++k) {
+            const long long b = ((long long)__builtin_amdgcn_readlane(hi, k) << 32) |
+                                (unsigned int)__builtin_amdgcn_readlane(lo, k);
+            cs = cs + __longlong_as_double(b);
+        }
+    }
+    return (cp - cs) / rii;
+}
+
+// Verification of one 16-row sub-panel of klein_mfma_kernel (32-row panels), run by
+// the whole wave when some lane has a decision the certificate did not cover
+// (bits of fl: sub-panel step s; bit 16: the sub-panel's sum |z| exceeded the
+// certificate's cap).  For each such lane L in turn, each uncovered decision is
+// redone at the reference-order mean (mu_exact_wave, plain decision, same uniform):
+// if every guess stands, only the skipped weight terms are added; otherwise (or
+// with bit 16) the whole sub-panel is replayed in the reference's order from the
+// weight and |z| sum of its start, rewriting L's coefficients and (OZ) history.
+// The decisions of lane L are computed redundantly by every lane (uniform inputs).
+// Returns the calling lane's weight; updates its |z| sum (z1l[lane]) and flags.
+template <bool WL, bool OZ, typename ZT>
+__device__ __noinline__ double verify_subpanel(const KleinArgs* __restrict__ A, ZT* __restrict__ Z, size_t ldz,
+                                               int64_t p0, int top, int rows, int fl, double lw,
+                                               uint32_t step, uint32_t chain, double* z1l,
+                                               const double* z1s, const double* lws, unsigned int& flags,
+                                               int& nz) {
+    const int lane = threadIdx.x & 63;
+    const int d = A->d;
+    // the sub-panel's coefficients / history were just stored by their own lanes and
+    // are read here by the whole wave: write back and invalidate this CU's L1
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    uint64_t todo = __builtin_amdgcn_ballot_w64(fl != 0);
+    while (todo) {
+        const int L = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const int flL = __builtin_amdgcn_readlane(fl, L);
+        const int64_t pL = p0 + L;
+        const int16_t* hL = OZ ? A->h16 + (size_t)pL * 16 : nullptr;
+        CoordStreamT<false> rs;
+        rs.init(A->seed, (uint32_t)__builtin_amdgcn_readlane((int)step, L),
+                (uint32_t)__builtin_amdgcn_readlane((int)chain, L));
+        // plain (reference-mode) decision of lane L's coordinate i at mean mu
+        auto decide = [&](int i, double mu, double& term, unsigned int& fb) -> double {
+            const double* q = A->szc ? A->szc + (size_t)i * kSzcStride : nullptr;
+            const double sg = q ? q[0] : A->sig[i];
+            const double u = rs.u((uint32_t)(d - 1 - i));
+            double zi = 0.0, ln = 0.0;
+            if (!isfinite(mu)) {
+                fb |= kFlagNonFinite;
+                term = 0.0;
+                return 0.0;
+            }
+            if (sg == 0.0) {
+                zi = rint(mu);
+            } else if (q) {
+                zi = sample_z_coord(mu, u, (gdptr)q, A->precision, A->linear_probs != 0, WL, (gdptr)A->etab, ln,
+                                    -1.0);
+            } else {
+                const SampleZOut o = sample_z(mu, sg, A->precision, A->linear_probs != 0, u, WL, A->etab);
+                zi = (double)o.z;
+                ln = o.log_norm;
+            }
+            term = WL ? ln : ref_weight(zi, mu, A->ros[i], A->isr[i], A->lterm[i]);
+            return zi;
+        };
+        auto guess = [&](int i) -> double {  // lane L's stored coefficient
+            if constexpr (OZ) {
+                const int ih = i + A->h16_shift;
+                return (double)((int)hL[(size_t)(ih >> 4) * A->h16_lanes * 16 + (ih & 15)] - 128);
+            } else {
+                return (double)Z[(size_t)i * ldz + pL];
+            }
+        };
+        bool full = (flL >> 16) & 1;
+        double dlw = 0.0;
+        unsigned int fb = 0;
+        for (int s = 0; s < rows && !full; ++s) {
+            if (!((flL >> s) & 1)) continue;
+            const int i = top - 1 - s;
+            const double mu = mu_exact_wave(A->R, hL, A->h16_lanes, A->h16_shift, Z + pL, ldz, i, d, A->cp[i], A->rii[i]);
+            double term;
+            const double zi = decide(i, mu, term, fb);
+            if (zi != guess(i)) full = true;
+            else dlw += term;
+        }
+        double z1n = 0.0;
+        int nzL = 0;
+        if (full) {  // replay the sub-panel from its start
+            dlw = 0.0;
+            z1n = z1s[L];
+            for (int s = 0; s < rows; ++s) {
+                const int i = top - 1 - s;
+                const double mu = mu_exact_wave(A->R, hL, A->h16_lanes, A->h16_shift, Z + pL, ldz, i, d, A->cp[i], A->rii[i]);
+                double term;
+                const double zi = decide(i, mu, term, fb);
+                dlw += term;
+                z1n += fabs(zi);
+                nzL |= zi != 0.0;
+                if (lane == L) {
+                    store_z(Z, (size_t)i * ldz + pL, zi, fb);
+                    if constexpr (OZ) {
+                        if (!(zi <= 32639.0 && zi >= -32767.0)) fb |= kFlagOverflow16;
+                        const int ih = i + A->h16_shift;
+                        A->h16[((size_t)(ih >> 4) * A->h16_lanes + pL) * 16 + (ih & 15)] =
+                            (int16_t)(int)(fmin(fmax(zi, -32767.0), 32639.0) + 128.0);
+                    }
+                }
+                // the wave's next reference-order sums read this coefficient
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+            }
+        }
+        if (lane == L) {
+            flags |= fb;
+            if (full) {
+                lw = lws[L] + dlw;
+                z1l[L] = z1n;
+                nz |= nzL;
+            } else {
+                lw += dlw;
+            }
+        }
+        if (lane == 0) atomicAdd(A->flags + kFlagWordResolved, 1u);
+    }
+    return lw;
+}
+
 // ------------------------------------------------------------ exact order
 template <typename ZT, bool WL>
 __global__ __launch_bounds__(256) void klein_exact_kernel(const KleinArgs a,
@@ -190,7 +437,7 @@ __global__ __launch_bounds__(256) void klein_exact_kernel(const KleinArgs a,
         double cs = 0.0;
         for (int j = i + 1; j < d; ++j) cs = cs + Ri[j] * (double)Z[(size_t)j * ldz + p];
         const double mu = (a.cp[i] - cs) / a.rii[i];
-        const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s);
+        const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s, -1.0);
         store_z(Z, (size_t)i * ldz + p, zi, flags);
     }
     if (a.LW) a.LW[p] = lw;
@@ -222,6 +469,7 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
     unsigned int flags = 0;
     const int npan = (d + PB - 1) / PB;
     double acc[PB];
+    double z1 = 0.0;  // sum of |z_j| decided so far (certificate)
     for (int pk = 0; pk < npan; ++pk) {
         const int p_hi = d - pk * PB;
         const int rows = p_hi < PB ? p_hi : PB;
@@ -247,7 +495,10 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
         for (int s = 0; s < rows; ++s) {
             const int i = p_hi - 1 - s;
             const double mu = (cst(a.cp)[i] - acc[PB - 1]) * cst(a.irii)[i];
-            const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s);
+            double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s,
+                                         cert_dmu(cst(a.cert)[2 * i], cst(a.cert)[2 * i + 1], z1, mu));
+            if (zi == kAmbiguous) zi = resolve_coord<WL>(a, i, Z + p, ldz, rs, lw, flags);
+            z1 += fabs(zi);
             store_z(Z, (size_t)i * ldz + p, zi, flags);
             const double x = zi;
             const cdptr rc = cst(RC) + (size_t)i * (PB - 1);
@@ -410,7 +661,6 @@ struct ZQuad<int64_t> {
 // VGPRs.  Row tile 1 (the upper sub-panel) goes to acc through the LDS tile;
 // tile 0 is parked in the per-wave scratch f0 and moved into the LDS tile once
 // the upper rows are loaded (the LDS tile is free during the upper sub-panel).
-typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
 #ifndef LGS_OZ_NG  // 16-sample groups per far-field pass (1 or 2)
 #define LGS_OZ_NG 2
 #endif
@@ -640,6 +890,19 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
     const int kq = lane >> 4, nq = lane & 15;
     constexpr int NACC = PB == 32 ? 16 : PB;  // running sums live across SampleZ calls
     double acc[NACC];
+    double z1 = 0.0;  // sum of |z_j| decided so far (certificate; 16-row panels)
+    // 32-row panels, per lane in LDS (a live register pair across the near field
+    // measured 0.7 ms slower per 2^20 samples): [0] the running sum of |z_j|, [1] it
+    // and [2] the weight at the start of the current sub-panel (for a replay)
+    __shared__ double cert_lds[3][PB == 32 ? 256 : 1];
+    // bit s: decision s of the current sub-panel not covered by the certificate (in
+    // LDS, written only when set: a live mask register costs ~13 scratch ops per
+    // coordinate at this kernel's register pressure)
+    __shared__ int cert_fl[PB == 32 ? 256 : 1];
+    if constexpr (PB == 32) {
+        cert_lds[0][threadIdx.x] = 0.0;
+        cert_fl[threadIdx.x] = 0;
+    }
     for (int pk = 0; pk < npan; ++pk) {
         const int p_hi = d - pk * PB;
         const int rows = p_hi < PB ? p_hi : PB;
@@ -772,9 +1035,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
             // still in flight at a SampleZ call would be waited for at the callee's
             // entry (the calling convention starts with s_waitcnt 0).
             bool pnz = false;  // (OZ) a nonzero coefficient in this panel, this lane
-            auto near16 = [&](int rows16, int top) {
+            auto near16 = [&](int rows16, int top) __attribute__((always_inline)) {
                 using ZH = std::conditional_t<sizeof(ZT) == 8, double, int>;
                 ZH zh[16];
+                cert_lds[1][threadIdx.x] = cert_lds[0][threadIdx.x];  // sum |z_j| before the sub-panel
+                cert_lds[2][threadIdx.x] = lw;
 #pragma unroll
                 for (int s = 0; s < 16; ++s) {
                     if (s < rows16) {
@@ -785,7 +1050,14 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         // no register moves per coordinate; 16 steps bring the map back
                         const double mu = (rec[kRecCp] - acc[(15 - s) & 15]) * rec[kRecIrii];
                         LGS_DC_T(t_sz0);
-                        const double zi = decide_coord_rec<WL>(a, i, mu, rec, rs, lw, flags, etab_s);
+                        // certified decision at the blocked-order mean (the |z| sum
+                        // bounded by the cap a.z1cap, checked after the sub-panel); a
+                        // decision not covered is a guess, verified after the sub-panel
+                        bool un;
+                        const double zi = decide_coord_rec<WL, true>(a, i, mu, rec, rs, lw, flags, etab_s,
+                                                                     cert_dmu(rec[kSzCa], rec[kSzCb], a.z1cap, mu),
+                                                                     un);
+                        if (un) cert_fl[threadIdx.x] |= 1 << s;
 #ifdef LGS_DIAG_CYCLES
                         {
                             LGS_DC_T(t_sz1);
@@ -849,6 +1121,25 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         hp[1] = h[1];
                     }
                 }
+                {
+                    // the certificate used sum_{j>i} |z_j| <= z1cap: verify it (the sum at
+                    // the sub-panel's end bounds every coordinate's) -- else replay
+                    double z1e = cert_lds[1][threadIdx.x];  // (re-read: not live across the sub-panel)
+#pragma unroll
+                    for (int s = 0; s < 16; ++s)
+                        if (s < rows16) z1e += fabs((double)zh[s]);
+                    cert_lds[0][threadIdx.x] = z1e;
+                }
+                const int fl = cert_fl[threadIdx.x] | (cert_lds[0][threadIdx.x] > a.z1cap ? (1 << 16) : 0);
+                if (__builtin_amdgcn_ballot_w64(fl != 0) != 0) {  // rare: verify / replay (whole wave)
+                    cert_fl[threadIdx.x] = 0;
+                    const int w64 = threadIdx.x & ~63;
+                    int nzv = 0;
+                    lw = verify_subpanel<WL, OZ>(&a, Z, ldz, p0, top, rows16, fl, lw, rs.step, rs.chain,
+                                                 &cert_lds[0][w64], &cert_lds[1][w64], &cert_lds[2][w64],
+                                                 flags, nzv);
+                    if constexpr (OZ) pnz |= nzv != 0;
+                }
             };
             near16(p_hi < 16 ? p_hi : 16, p_hi);
             const int rows_l = p_hi - 16 < 16 ? p_hi - 16 : 16;
@@ -890,7 +1181,10 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
             for (int s = 0; s < rows; ++s) {
                 const int i = p_hi - 1 - s;
                 const double mu = (cst(a.cp)[i] - acc[PB - 1]) * cst(a.irii)[i];
-                const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s);
+                double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s,
+                                             cert_dmu(cst(a.cert)[2 * i], cst(a.cert)[2 * i + 1], z1, mu));
+                if (zi == kAmbiguous) zi = resolve_coord<WL>(a, i, Z + p, ldz, rs, lw, flags);
+                z1 += fabs(zi);
                 store_z(Z, (size_t)i * ldz + p, zi, flags);
                 const double x = zi;
                 const cdptr rc = cst(RC) + (size_t)i * (PB - 1);
@@ -901,6 +1195,12 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                 acc[0] = 0.0;
             }
         }
+    }
+    if constexpr (PB == 32) {  // the largest sum |z_j| of the wave -> the context's cap
+        double m = active ? cert_lds[0][threadIdx.x] : 0.0;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+        if (lane == 0 && a.z1max) atomicMax(a.z1max, (unsigned long long)__double_as_longlong(m));
     }
     if (!active) return;
     if (a.LW) a.LW[p] = lw;

@@ -61,6 +61,10 @@ inline void build_szc(double s, int precision, double* q) {
     q[6] = rf * s;
     if (s < 4.0) {
         q[2] = lgs::kSzSmall;
+        // a point entering / leaving at a window end lies >= q6 + 1 from mu while a
+        // window point lies within 1/2: relative mass <= exp(-((q6+1)^2 - 1/4) / (2 s^2))
+        const double e = ((q[6] + 1.0) * (q[6] + 1.0) - 0.25) / (2.0 * s * s);
+        q[7] = e > 42.0 ? 0.0 : 1.0;  // 2^-60 = e^-41.6
         return;
     }
     const double W = 2.0 * q[6];

@@ -37,13 +37,15 @@ LGS_X_I64 = 0x200
 
 KERNEL_KLEIN, KERNEL_BZ, KERNEL_ACCEPT, KERNEL_MOMENTS = 0, 1, 2, 3
 KERNEL_GRAM, KERNEL_SERIES = 4, 5
+LGS_COUNTER_RESOLVED = 0
+LGS_COUNTER_FALLBACK = 1
 
 # every symbol include/lgs.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_destroy", "lgs_set_stream",
            "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_lattice_points", "lgs_log_density", "lgs_sample_z", "lgs_timing_enable",
            "lgs_timing_get", "lgs_device_info", "lgs_series_stats", "lgs_gram",
            "lgs_jump_distance", "lgs_marginal_tvd", "lgs_set_decoder", "lgs_nearest_plane",
-           "lgs_round_decode")
+           "lgs_round_decode", "lgs_counter")
 
 
 class LgsError(RuntimeError):
@@ -94,6 +96,7 @@ def load_library(path: str = LIB_PATH):
                                ctypes.c_uint32]
     L.lgs_timing_enable.argtypes = [_vp, ctypes.c_int]
     L.lgs_timing_get.argtypes = [_vp, ctypes.c_int, _dp, _i64p]
+    L.lgs_counter.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
     L.lgs_device_info.argtypes = [_vp, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                   _i64p]
     _i64 = ctypes.c_int64
@@ -328,6 +331,19 @@ class Context:
         n = ctypes.c_int64(0)
         _check(_lib.lgs_timing_get(self._h, int(kernel), ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+    def resolved(self, reset=False):
+        """Decisions the certificate did not cover and that were redone at the
+        reference-order mean (LGS_COUNTER_RESOLVED), since creation / the last reset."""
+        v = ctypes.c_uint64(0)
+        _check(_lib.lgs_counter(self._h, LGS_COUNTER_RESOLVED, 1 if reset else 0, ctypes.byref(v)))
+        return v.value
+
+    def fallbacks(self, reset=False):
+        """Klein launches redone with a wider store / the fp64 far field (LGS_COUNTER_FALLBACK)."""
+        v = ctypes.c_uint64(0)
+        _check(_lib.lgs_counter(self._h, LGS_COUNTER_FALLBACK, 1 if reset else 0, ctypes.byref(v)))
+        return v.value
 
     def device_info(self):
         buf = ctypes.create_string_buffer(256)

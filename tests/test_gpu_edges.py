@@ -71,6 +71,26 @@ def test_exact_order_on_ill_conditioned_basis(ctx, oracle):
     assert np.array_equal(r["z"], o["z"])
 
 
+@pytest.mark.parametrize("n", [256, 128, 130])
+def test_certified_default_order_on_ill_conditioned_basis(capi, oracle, n):
+    """The default blocked kernels certify every decision against a bound on
+    |mu_blocked - mu_reference| and redo the uncovered ones at the reference-order
+    mean (lgs_device.h, certified decisions), so they are bit-exact on the same
+    basis where half the samples used to change.  n = 256: int8-digit
+    far field (which hands over to the fp64 far field once |z| > 32639), 128: fp64
+    MFMA far field, 130: VALU panel kernel (ragged launch)."""
+    ctx = capi.Context(0)  # fresh: the |z| > 32639 hand-over is sticky per context
+    B = _ill_basis(64, 64)
+    R, cp = oracle.qr_prepare(B)
+    ctx.set_basis(R, cp, B, 3.5)
+    ctx.resolved(reset=True)
+    r = ctx.klein_host(841, 31, n, want_z=True, want_v=False)
+    o = oracle.klein(R, cp, 3.5, n, seed=841, first_sample=31, B=B)
+    assert np.abs(o["z"]).max() > 1 << 40
+    assert np.array_equal(r["z"], o["z"])
+    assert ctx.resolved() > 0  # the certificate declined some decisions here
+
+
 def test_klein_empty(ctx, oracle, capi):
     B = _int_basis(33, 1)
     R, cp = oracle.qr_prepare(B)
