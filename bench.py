@@ -6,21 +6,35 @@ sigma = 165.7, IMHK with 2^14 chains per GPU.  One bench step = one
 ``lgs_imhk`` call advancing every chain by --imhk-steps steps: 2^14 x 64 =
 2^20 Klein proposals (back-substitution + SampleZ + importance weight), the
 Metropolis scan, exact integer moments, and the lattice points v = B z of every
-kept state (thin = 1), all resident in HBM.  value = Klein proposals per second
-over all ranks (weak scaling: chains per GPU fixed).
+kept state (thin = 1), all resident in HBM; then the lag-L autocovariance sums
+of two scalar functionals of the kept states (a coefficient and ||v||^2, SURVEY
+§8e) are accumulated on the device.  The coefficient is z_{d-1}, the first one
+Klein decides (for the NTRU / q-ary bases z_0 is a q-coordinate with sigma_0 ~
+0.01, identically 0).  value = Klein proposals per second over all ranks
+(weak scaling: chains per GPU fixed).
 
-Multi-GPU: launched by torch.distributed.run; rank r owns chains
-[r * 2^14, (r+1) * 2^14) (global chain ids -> Philox counters), so the union of
-all ranks' chains is bit-identical for any GPU count.  The only collective is
-one RCCL all-reduce of the moment / acceptance accumulators per step.
+Multi-GPU: ``python bench.py --gpus N`` (no WORLD_SIZE in the environment)
+starts ``torch.distributed.run`` with N ranks as a child process and exits with
+its status; rank r owns chains [r * C, (r+1) * C) (global chain ids -> Philox
+counters), so the union of all ranks' chains is bit-identical for any GPU
+count.  The one exchange is a single RCCL all-reduce after the timed steps of
+every accumulator (acceptance, exact moments, the lag sums), inside the timed
+region.  The 8-GPU workload of BASELINE configs[3] is
+``--gpus 8 --config C4_qary1024`` (2^15 chains per GPU, 2^18 in all).
 
-Also reported: roofline of the dominant kernel (the Klein sampler, HIP-event
-timed on its launch stream), IMHK acceptance next to the CPU reference's, and
-the CPU baseline (the C oracle, OpenMP over the host cores, bounded sample).
+Also reported: the dominant kernel's roofline (the Klein sampler, HIP-event
+timed on its launch stream; executed-work and HBM counters from the committed
+rocprofv3 profile of this command, profiles/r02*_klein_counters.json), the
+certificate's redo count, a parity check of the timed run's final chain states
+against the oracle, and the CPU baselines (the C oracle over the host cores and
+the NumPy restatement of the reference's loop, one process per core).
 """
 import argparse
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,6 +46,53 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector / matrix dense peak (spec)
+I8_PEAK_TOPS = 5000.0      # MI355X int8 MFMA dense (2x BF16 per clock, MI355X_MICROARCH.md)
+ACF_LAGS = 16              # lag-L autocovariance of z_{d-1} and ||v||^2
+ACF_CHAINS = 1024          # chains per rank whose states feed the lag sums
+
+WORKLOADS = {
+    "C3_ntru512": dict(chains=1 << 14, text="NTRU n=512 q=12289 d=1024 sigma=165.7 IMHK"),
+    "C4_qary1024": dict(chains=1 << 15, text="q-ary d=1024 k=512 q=3329 sigma=165.7 IMHK (8 GPUs: 2^18 chains)"),
+    "C2_qary128": dict(chains=1 << 16, text="q-ary d=128 q=3329 sigma=165.7 IMHK"),
+    "C5_ntru2048": dict(chains=1 << 12, text="NTRU n=2048 q=12289 d=4096 sigma=165.7 IMHK (fp64 throughout)"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C3_ntru512", choices=sorted(WORKLOADS))
+    ap.add_argument("--chains", type=int, default=0, help="IMHK chains per GPU (default per config)")
+    ap.add_argument("--imhk-steps", type=int, default=64, help="IMHK steps per bench step (one lgs_imhk call)")
+    ap.add_argument("--no-v", action="store_true", help="skip lattice points (coefficients only)")
+    ap.add_argument("--exact-order", action="store_true")
+    ap.add_argument("--cpu-samples", type=int, default=0, help="IMHK proposals for the C-oracle baseline")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--numpy-samples", type=int, default=24, help="Klein samples per process, NumPy baseline")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--counters", default=os.environ.get("LGS_COUNTERS_JSON", ""),
+                    help="klein_counters.json of a rocprofv3 profile of this command (default: newest in profiles/)")
+    return ap.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """--gpus N without a torch.distributed launcher: N ranks as a child process
+    (never an exec: nothing here has touched the GPU yet); rank 0 prints the line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 def _cpu_model():
@@ -45,65 +106,112 @@ def _cpu_model():
     return None
 
 
+def cpu_share():
+    """CPUs this process may use: its affinity set, capped by OMP_NUM_THREADS (the
+    GPU box exports its per-GPU CPU share there)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(n, 1)
+
+
 def b_alg(d):
-    """Algorithmic bytes per Klein sample: fp64 upper triangle of R + int32 z."""
+    """SURVEY §8d algorithmic bytes per Klein sample: fp64 upper triangle of R + int32 z
+    (R counted once per sample -- it is shared by every chain, see roofline notes)."""
     return 8 * d * (d + 1) // 2 + 4 * d
 
 
-def parse():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C3_ntru512")
-    ap.add_argument("--chains", type=int, default=1 << 14, help="IMHK chains per GPU")
-    ap.add_argument("--imhk-steps", type=int, default=64, help="IMHK steps per bench step (one lgs_imhk call)")
-    ap.add_argument("--no-v", action="store_true", help="skip lattice points (coefficients only)")
-    ap.add_argument("--exact-order", action="store_true")
-    ap.add_argument("--cpu-samples", type=int, default=16384, help="IMHK proposals for the CPU baseline")
-    ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic-csv", default=os.environ.get(
-                        "LGS_TRAFFIC_CSV", os.path.join(REPO, "profiles", "r01n_pmc_klein.csv")),
-                    help="rocprofv3 --pmc counter_collection.csv with FETCH_SIZE/WRITE_SIZE")
-    return ap.parse_args()
-
-
-def pmc_traffic(path, kernel_substr="klein_"):
-    """Per-launch HBM bytes of the Klein kernel from rocprofv3 --pmc CSVs.
-
-    `path` is a counter_collection.csv holding FETCH_SIZE and/or WRITE_SIZE rows
-    (tools/gpu_prof.sh collects them in separate passes and tools/summarize_prof.py
-    merges the Klein-kernel rows).  Only the largest dispatches (the bench's main
-    launches) are averaged.  FETCH_SIZE / WRITE_SIZE are in KB; on gfx950
-    FETCH_SIZE reports half of a wide coalesced read (MI355X_MICROARCH.md §HBM),
-    so it is doubled."""
-    import csv
+def load_counters(path, config):
+    """Per-launch Klein-kernel counters of a rocprofv3 profile of this bench command
+    (tools/gpu_roofline.sh -> profiles/<tag>_klein_counters.json)."""
+    if not path:
+        cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r02*_klein_counters.json")))
+        cands = [c for c in cands if json.load(open(c)).get("config") == config]
+        path = cands[-1] if cands else ""
     if not path or not os.path.exists(path):
-        return None
-    rows = [r for r in csv.DictReader(open(path)) if kernel_substr in r.get("Kernel_Name", "")]
-    if not rows:
-        return None
-    gmax = max(int(r["Grid_Size"]) for r in rows)
-    vals = {}
-    for r in rows:
-        if int(r["Grid_Size"]) == gmax:
-            vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    if "FETCH_SIZE" not in vals:
-        return None
-    fetch = 2.0 * 1024 * sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
-    write = 1024 * sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"]) if "WRITE_SIZE" in vals else 0.0
-    return fetch + write
+        return None, None
+    return json.load(open(path)), os.path.relpath(path, REPO)
+
+
+class LagSums:
+    """Lag-L autocovariance sums of per-chain scalar series, continued across bench
+    steps through a ring of each chain's last L values.  int64 sums
+    (exact, order-independent) for integer series, fp64 otherwise."""
+
+    def __init__(self, torch, n_chains, L, dtype, device):
+        self.t, self.L = torch, L
+        self.ring = torch.zeros((n_chains, L), dtype=dtype, device=device)
+        self.have = 0
+        self.S = torch.zeros(L + 1, dtype=dtype, device=device)   # sum_t x_t x_{t-k}
+        self.N = torch.zeros(L + 1, dtype=torch.int64, device=device)  # pairs per lag
+        self.S1 = torch.zeros(1, dtype=dtype, device=device)
+        self.n = torch.zeros(1, dtype=torch.int64, device=device)
+
+    def update(self, x):
+        torch, L, h = self.t, self.L, self.have
+        nc, T = x.shape
+        xs = torch.cat([self.ring[:, L - h:], x], 1)
+        for k in range(L + 1):
+            t0 = max(0, k - h)
+            if t0 >= T:
+                continue
+            self.S[k] += (x[:, t0:] * xs[:, h + t0 - k:h + T - k]).sum()
+            self.N[k] += nc * (T - t0)
+        self.S1 += x.sum()
+        self.n += x.numel()
+        keep = min(L, h + T)
+        self.ring[:, L - keep:] = xs[:, xs.shape[1] - keep:]
+        self.have = keep
+
+    def parts(self):
+        return [self.S, self.N, self.S1, self.n]
+
+    @staticmethod
+    def acf(S, N, S1, n):
+        """ACF_k = (mean of lag-k products - mean^2) / (mean of squares - mean^2)."""
+        m = S1 / n
+        c = S / np.maximum(N, 1) - m * m
+        return (c / c[0]).tolist() if c[0] > 0 else None
+
+
+def pack_f64(torch, parts):
+    """One fp64 tensor for the single all-reduce: int64 parts split into exact
+    32-bit halves (each sum of halves over <= 2^20 ranks stays below 2^53)."""
+    out, layout = [], []
+    for p in parts:
+        if p.dtype == torch.int64:
+            out += [(p >> 32).double(), (p & 0xFFFFFFFF).double()]
+            layout.append(("i", p.numel()))
+        else:
+            out.append(p.double())
+            layout.append(("f", p.numel()))
+    return torch.cat(out), layout
+
+
+def unpack_f64(torch, flat, layout):
+    res, o = [], 0
+    for kind, n in layout:
+        if kind == "i":
+            hi, lo = flat[o:o + n], flat[o + n:o + 2 * n]
+            res.append((hi.round().long() << 32) + lo.round().long())
+            o += 2 * n
+        else:
+            res.append(flat[o:o + n])
+            o += n
+    return res
 
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     import torch
     import torch.distributed as dist
     from lgs_amd import _capi
-    from lgs_amd.lattices import CONFIGS, build_config
+    from lgs_amd.lattices import build_config
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("LGS_ONE_DEVICE") == "1":  # rehearsal: every rank on device 0 (gloo)
@@ -121,14 +229,16 @@ def main():
     B = lat.basis
     d = B.shape[0]
     # host QR set-up of klein.py:56-79 (identical to the drop-in)
-    Q, R = np.linalg.qr(B, mode="full")
+    Q, R = np.linalg.qr(B, mode="complete")
     sgn = np.where(np.diag(R) < 0, -1.0, 1.0)
     R = np.ascontiguousarray(R * sgn[:, None])
     cp = np.zeros(d)
+    binv_k = np.linalg.inv(B)[d - 1]  # z_{d-1} = row d-1 of B^-1 times v (rounded: v, z integral)
 
     ctx = _capi.Context(local)
     ctx.set_basis(R, cp, B, sigma)
-    nc, T = args.chains, args.imhk_steps
+    nc = args.chains or WORKLOADS[args.config]["chains"]
+    T = args.imhk_steps
     first_chain = rank * nc
     seed = 0x5EED_0001
     flags = _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR
@@ -140,6 +250,10 @@ def main():
     acc = torch.zeros(nc, dtype=torch.int64, device=dev)
     mom = torch.zeros(2 * d, dtype=torch.int64, device=dev)
     v_samples = None if args.no_v else torch.empty((nc, T, d), dtype=torch.float64, device=dev)
+    nacf = min(nc, ACF_CHAINS)
+    binv_t = torch.from_numpy(binv_k).to(dev)
+    lag_z0 = LagSums(torch, nacf, ACF_LAGS, torch.int64, dev)
+    lag_vv = LagSums(torch, nacf, ACF_LAGS, torch.float64, dev)
     torch.cuda.synchronize()
 
     step_counter = [1]
@@ -148,18 +262,24 @@ def main():
         ctx.imhk(seed, first_chain, nc, step_counter[0], T, 1, z_state, lw, init, acc,
                  v_samples=v_samples, moments=mom, flags=flags)
         step_counter[0] += T
+        if v_samples is not None:
+            vs = v_samples[:nacf]
+            lag_z0.update(torch.round(vs @ binv_t).long())
+            lag_vv.update((vs * vs).sum(-1) * 1e-6)
 
     def reduce_stats():
-        stats = torch.cat([acc.sum().reshape(1), mom])  # per-rank accumulators
+        flat, layout = pack_f64(torch, [acc.sum().reshape(1), mom] + lag_z0.parts() + lag_vv.parts())
         if world > 1:
-            dist.all_reduce(stats)  # the single RCCL collective over xGMI
-        return stats
+            dist.all_reduce(flat)  # the single collective (RCCL over xGMI)
+        return unpack_f64(torch, flat, layout)
 
     for _ in range(args.warmup):
         one_step()
     reduce_stats()  # warm torch's lazily loaded kernels and the communicator
     acc.zero_()
     mom.zero_()
+    lag_z0 = LagSums(torch, nacf, ACF_LAGS, torch.int64, dev)
+    lag_vv = LagSums(torch, nacf, ACF_LAGS, torch.float64, dev)
     ctx.resolved(reset=True)
     ctx.timing_enable(True)
     torch.cuda.synchronize()
@@ -184,69 +304,106 @@ def main():
     g_ms, g_n = ctx.timing_get(_capi.KERNEL_BZ)
     a_ms, a_n = ctx.timing_get(_capi.KERNEL_ACCEPT)
     m_ms, m_n = ctx.timing_get(_capi.KERNEL_MOMENTS)
-    acceptance = float(stats[0].item()) / proposals
     redos = ctx.resolved()
+    s_acc = int(stats[0].item())
+    acceptance = s_acc / proposals
+    sz = [x.cpu().numpy() for x in stats[2:6]]
+    sv = [x.cpu().numpy() for x in stats[6:10]]
+    acf = {"lags": ACF_LAGS, "chains": nacf * world,
+           "z_last": LagSums.acf(sz[0].astype(np.float64), sz[1], float(sz[2][0]), float(sz[3][0])),
+           "norm_v_sq": LagSums.acf(sv[0], sv[1], float(sv[2][0]), float(sv[3][0]))}
+
+    # ---- parity: the timed run's final chain states against the oracle.  In the
+    # reference's IMHK mode every proposal is accepted (the weight is a constant up to
+    # rounding, imhk.py:102-124), so chain c's state is its last proposal: the Klein
+    # sample at counter (chain first_chain + c, step step_counter - 1).
+    import lgs_oracle
+    parity = None
+    if rank == 0:
+        zs = z_state.cpu().numpy()
+        last = step_counter[0] - 1
+        chk = [int(c) for c in np.linspace(0, nc - 1, 8)]
+        if acceptance == 1.0:
+            ok = 0
+            for c in chk:
+                o = lgs_oracle.klein(R, cp, sigma, 1, seed=seed, first_sample=(last << 32) | (first_chain + c))
+                ok += int(np.array_equal(zs[:, c], o["z"][0]))
+            parity = f"{ok}/{len(chk)} final chain states (after {step_counter[0] - 1} IMHK steps) bit-exact vs oracle"
+        else:
+            parity = "skipped: acceptance < 1 (final state is not the last proposal)"
 
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
 
-    # ---- roofline of the dominant kernel (the Klein sampler), HIP-event timed on its
-    # launch stream.  It is FP64-compute bound: algorithmic work = d^2 flops per
-    # sample (the d^2/2 multiply-adds of klein.py:191-193), peak = FP64 dense
-    # (vector = matrix = 78.6 TF spec on MI355X).  The north_star's HBM view
-    # (B_alg bytes per sample) is reported beside it.
+    # ---- roofline of the dominant kernel (the Klein sampler), HIP-event timed on
+    # its launch stream.  The kernel is bound by neither pipe nor HBM: it issues the
+    # near-field fp64 FMAs and SampleZ's fp64 polynomials on the VALU (the FP64
+    # datapath it shares with fp64 MFMA), the far field on int8 MFMA, and waits on
+    # latency.  Executed work comes from SQ counters of the committed profile of this
+    # command (per launch), so every fraction is of work actually issued.
     units = nc * T
     k_avg_s = (k_ms / max(k_n, 1)) / 1e3
-    tflops = units * float(d) * d / k_avg_s / 1e12
-    traffic = pmc_traffic(args.traffic_csv, kernel_substr="klein_")
-    roofline = {"bound": "mfma", "achieved": round(tflops, 3), "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(tflops / FP64_PEAK_TFLOPS, 4),
-                "traffic": None if traffic is None else round(traffic),
-                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
-                "kernel": "klein_exact_kernel" if args.exact_order else "klein_mfma_kernel",
-                "kernel_ms_avg": round(k_avg_s * 1e3, 3), "units_per_launch": units,
-                "flops_per_unit": d * d,
-                "hbm_algorithmic": {"bytes_per_unit": b_alg(d),
-                                    "achieved_GBs": round(units * b_alg(d) / k_avg_s / 1e9, 1),
-                                    "frac_of_8TBs": round(units * b_alg(d) / k_avg_s / 1e9 / HBM_PEAK_GBS, 3)}}
+    cnt, cnt_path = load_counters(args.counters, args.config)
+    roofline = {"bound": "mfma", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS, "achieved": None, "frac": None,
+                "traffic": None, "kernel": "klein_exact_kernel" if args.exact_order else "klein_mfma_kernel",
+                "kernel_ms_avg": round(k_avg_s * 1e3, 3), "units_per_launch": units}
+    if cnt and cnt.get("units_per_launch") == units:
+        f64 = cnt["fp64_flops"]
+        roofline.update({
+            "achieved": round(f64 / k_avg_s / 1e12, 3), "frac": round(f64 / k_avg_s / 1e12 / FP64_PEAK_TFLOPS, 4),
+            "what": "executed fp64 flops (VALU FMA x2 + ADD/MUL + fp64 MFMA) per launch / launch time; FP64 pipe peak",
+            "traffic": int(cnt["hbm_bytes"]),
+            "traffic_note": "FETCH_SIZE x2 + WRITE_SIZE per launch (gfx950 correction), profile of this command",
+            "hbm": {"achieved_GBs": round(cnt["hbm_bytes"] / k_avg_s / 1e9, 1),
+                    "frac_of_8TBs": round(cnt["hbm_bytes"] / k_avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                    "compulsory_bytes": int(cnt["compulsory_bytes"]),
+                    "traffic_over_compulsory": round(cnt["hbm_bytes"] / cnt["compulsory_bytes"], 2)},
+            "int8_mfma": {"achieved_TOPS": round(cnt["i8_ops"] / k_avg_s / 1e12, 2),
+                          "frac_of_5POPS": round(cnt["i8_ops"] / k_avg_s / 1e12 / I8_PEAK_TOPS, 4)},
+            "issue": cnt["issue"],
+            "counters": cnt_path})
+    roofline["hbm_algorithmic_note"] = (
+        f"SURVEY 8d B_alg = {b_alg(d)} B/sample counts R once per sample, but R is shared by every "
+        f"chain (read once per 256-sample block from L2), so B_alg x rate is not an HBM quantity")
     gemm = None
     if g_n:
-        # B z over all proposals + the carried states: 2 d^2 flops per vector
-        gemm = {"kernel": "bz_gemm_kernel" if os.environ.get("LGS_BZ_FP64") == "1" else "bz_i8_kernel", "ms_per_step": round(g_ms / args.steps, 3),
-                "tflops": round(2.0 * d * d * (units + nc) * args.steps / (g_ms / 1e3) / 1e12, 2)}
+        gemm = {"kernel": "bz_gemm_kernel" if os.environ.get("LGS_BZ_FP64") == "1" else "bz_i8_kernel",
+                "ms_per_step": round(g_ms / args.steps, 3)}
 
-    # ---- parity spot check of this run's first proposals against the oracle
-    import lgs_oracle
-    n_chk = 8
-    zc = torch.empty((d, n_chk), dtype=torch.int32, device=dev)
-    ctx.klein(seed, 0, n_chk, zc, None, None, flags)
-    o = lgs_oracle.klein(R, cp, sigma, n_chk, seed=seed, first_sample=0)
-    parity = int((zc.cpu().numpy().T == o["z"]).all(1).sum())
-
-    # ---- CPU baseline: the C oracle (IMHK reference mode), OpenMP over host cores
+    # ---- CPU baselines (bounded samples; rank 0 at N=1 only)
     cpu = None
     if world == 1 and not args.no_cpu:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        n_ch = max(threads, 1)
-        steps_cpu = max(1, args.cpu_samples // n_ch)
+        threads = args.cpu_threads or cpu_share()
+        n_ch = threads
+        cpu_props = args.cpu_samples or 512 * threads
+        steps_cpu = max(1, cpu_props // n_ch)
         t1 = time.perf_counter()
         zc_, lwc, accc = lgs_oracle.imhk_parallel(R, cp, B, sigma, n_ch, steps_cpu, seed=seed,
                                                   first_step=1, threads=threads)
         tc = time.perf_counter() - t1
         props = n_ch * (steps_cpu + 1)  # + the initial draw of every chain
-        cpu = {"value": round(props / tc, 2), "unit": "Klein samples/s", "cores": threads,
-               "kind": "port",
-               "sample": f"{n_ch} IMHK chains x {steps_cpu} steps (+1 initial draw), same NTRU "
-                         f"d={d} basis, reference-mode weights, {tc:.1f} s wall on {threads} threads",
+        cpu = {"value": round(props / tc, 2), "unit": "Klein samples/s", "cores": threads, "kind": "port",
+               "sample": f"C oracle (lgs_oracle.c, OpenMP): {n_ch} IMHK chains x {steps_cpu} steps (+1 initial "
+                         f"draw), same basis, reference-mode weights, {tc:.1f} s wall on {threads} threads",
                "acceptance": float(accc.sum() / (n_ch * steps_cpu)),
                "per_core": round(props / tc / threads, 2), "host_cpus": os.cpu_count(),
                "cpu_model": _cpu_model()}
+        if args.numpy_samples > 0:
+            import lgs_numpy_restatement as NR
+            rate, tot, wall = NR.timed_run(R, cp, B, sigma, processes=threads,
+                                           samples_per_process=args.numpy_samples, seed=seed)
+            cpu["numpy_restatement"] = {
+                "value": round(rate, 2), "unit": "Klein samples/s", "cores": threads,
+                "per_core": round(rate / threads, 3),
+                "sample": f"{tot} Klein samples of the reference's NumPy loop (klein.py:101-220), "
+                          f"{threads} processes x {args.numpy_samples}, {wall:.1f} s per process"}
 
     dinfo = ctx.device_info()
     out = {
-        "metric": "Klein samples/sec at n=512 NTRU (IMHK proposals, d=1024)",
+        "metric": "Klein samples/sec at n=512 NTRU (IMHK proposals, d=1024)" if args.config == "C3_ntru512"
+        else f"Klein samples/sec, {args.config} (IMHK proposals, d={d})",
         "value": round(value, 1),
         "unit": "samples/s",
         "n_gpus": world,
@@ -257,15 +414,17 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (Philox-generated NTRU public key h, seed 1)",
-        "config": {"workload": f"{args.config}: NTRU n=512 q=12289 d={d} sigma={sigma} IMHK",
-                   "chains_per_gpu": nc, "imhk_steps_per_step": T, "thin": 1,
-                   "lattice_points": not args.no_v, "kernel_order": "exact" if args.exact_order else "panel",
-                   "parallelism": f"chains sharded over {world} GPU(s), 1 RCCL all-reduce per step"},
+        "data": "synthetic (Philox-generated basis, seed 1)",
+        "config": {"workload": f"{args.config}: {WORKLOADS[args.config]['text']}",
+                   "chains_per_gpu": nc, "chains_total": nc * world, "imhk_steps_per_step": T, "thin": 1,
+                   "lattice_points": not args.no_v, "kernel_order": "exact" if args.exact_order else "certified-blocked",
+                   "parallelism": f"chains sharded over {world} GPU(s); one RCCL all-reduce of every accumulator "
+                                  f"after the timed steps (inside the timed region)"},
         "imhk_acceptance": round(acceptance, 6),
-        "imhk_acceptance_cpu_reference": 1.0,
-        "parity_check": f"{parity}/{n_chk} proposals bit-exact vs oracle",
-        "certificate_redos": {"coordinates": redos, "per_proposal": redos / (args.steps * nc * T)},
+        "imhk_acceptance_cpu_reference": None if cpu is None else cpu["acceptance"],
+        "parity_check": parity,
+        "certificate_redos": {"verified_subpanels": redos, "per_proposal": redos / (args.steps * nc * T)},
+        "autocorrelation": acf,
         "roofline": roofline,
         "gemm": gemm,
         "kernel_ms": {"klein": round(k_ms / max(k_n, 1), 3), "bz": round(g_ms / max(g_n, 1), 3),

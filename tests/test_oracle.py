@@ -139,3 +139,18 @@ def test_oracle_wang_ling_weight_is_log_normaliser_sum(oracle):
         k = np.arange(lo, lo + n)
         acc += scipy.special.logsumexp(-0.5 * ((k - mu) / s) ** 2)
     assert lw == pytest.approx(acc, rel=1e-10)
+
+
+def test_numpy_restatement_matches_oracle(oracle):
+    """The NumPy restatement timed as bench.py's second CPU baseline (the reference's
+    loop structure, klein.py:101-220) draws the oracle's lattice points."""
+    import lgs_numpy_restatement as NR
+    rng = np.random.default_rng(12)
+    B = 5 * np.eye(12) + rng.integers(-2, 3, (12, 12))
+    R, cp = oracle.qr_prepare(B)
+    nk = NR.NumpyKlein(R, cp, B, 3.0)
+    seed = 77
+    for c in range(6):
+        v = nk.sample_single(lambda slot, c=c: oracle.philox_u(seed, slot, 0, c, 0))
+        o = oracle.klein(R, cp, 3.0, 1, seed=seed, first_sample=c, B=B)
+        np.testing.assert_array_equal(v, o["v"][0])

@@ -1,0 +1,55 @@
+"""Per-launch Klein-kernel counters of a rocprofv3 profile of bench.py -> JSON for
+bench.py's roofline (tools/gpu_roofline.sh).
+
+usage: roofline_counters.py <profile dir> <config> <units_per_launch> <d> <out.json>
+
+Every counter_collection.csv under the profile dir is read; rows of the Klein
+kernel's largest dispatches (the bench's 2^20-proposal launches) are averaged per
+counter.  Executed fp64 flops = 64 lanes x (2 FMA + MUL + ADD) fp64 VALU
+instructions + 2048 flops per v_mfma_f64_16x16x4 (the near-field coupling: 16 per
+32-row panel per wave; the far field runs on int8); int8 ops = 32768 per
+v_mfma_i32_16x16x64_i8 (all other MFMA instructions).  HBM bytes = FETCH_SIZE x 2
++ WRITE_SIZE (KB; gfx950 correction, MI355X_MICROARCH.md).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+root, config, units, d, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+vals = defaultdict(list)
+grid_max = 0
+rows_all = []
+for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "klein_mfma_kernel" in r.get("Kernel_Name", ""):
+            rows_all.append(r)
+            grid_max = max(grid_max, int(r["Grid_Size"]))
+disp = defaultdict(lambda: defaultdict(float))
+for r in rows_all:
+    if int(r["Grid_Size"]) == grid_max:
+        disp[(r["Counter_Name"], r["Dispatch_Id"], r.get("Agent_Id", ""))]["v"] += float(r["Counter_Value"])
+for (name, _, _), v in disp.items():
+    vals[name].append(v["v"])
+avg = {k: sum(v) / len(v) for k, v in vals.items()}
+waves = avg.get("SQ_WAVES")
+n_panels = (d + 31) // 32
+f64_mfma = (waves or 0) * 16 * max(n_panels - 1, 0)
+res = {"config": config, "units_per_launch": units, "grid_size": grid_max,
+       "counters_per_launch": avg,
+       "fp64_flops": 64 * (2 * avg.get("SQ_INSTS_VALU_FMA_F64", 0) + avg.get("SQ_INSTS_VALU_MUL_F64", 0)
+                           + avg.get("SQ_INSTS_VALU_ADD_F64", 0)) + 2048 * f64_mfma,
+       "i8_ops": 32768 * max(avg.get("SQ_INSTS_MFMA", 0) - f64_mfma, 0),
+       "hbm_bytes": 1024 * (2 * avg.get("FETCH_SIZE", 0) + avg.get("WRITE_SIZE", 0)),
+       "compulsory_bytes": units * d * 2 + 8 * d * (d + 1) // 2}
+wc = avg.get("SQ_WAVE_CYCLES")
+if wc:
+    res["issue"] = {"valu_active_per_wave_cycle": round(avg.get("SQ_ACTIVE_INST_VALU", 0) / wc, 4),
+                    "any_active_per_wave_cycle": round(avg.get("SQ_ACTIVE_INST_ANY", 0) / wc, 4),
+                    "waiting_on_memory_or_barrier": round(avg.get("SQ_WAIT_ANY", 0) / wc, 4),
+                    "waiting_on_issue": round(avg.get("SQ_WAIT_INST_ANY", 0) / wc, 4),
+                    "valu_insts_per_wave": round(avg.get("SQ_INSTS_VALU", 0) / (waves or 1), 1)}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps({k: v for k, v in res.items() if k != "counters_per_launch"}))
