@@ -103,7 +103,9 @@ __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double
 }
 
 // decide_coord with the coordinate's record rec staged in LDS (klein_mfma_kernel, 32-row panels).
-template <bool WL, bool CERT, typename TP>
+// LIBM: the SampleZ path without per-coordinate constants (LGS_SAMPLEZ_LIBM); a
+// separate kernel instantiation, so the default kernel carries one call path.
+template <bool WL, bool CERT, bool LIBM, typename TP>
 __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, double mu,
                                                    lds_cdptr rec, CoordStream& rs, double& lw,
                                                    unsigned int& flags, TP etab, double dmu, bool& amb) {
@@ -131,7 +133,7 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
     if (s == 0.0) {
         zi = rint(mu);
         amb = CERT && !round_stable(mu, dmu);
-    } else if (!a.szc) {  // LGS_SAMPLEZ_LIBM: generic path
+    } else if (LIBM) {  // LGS_SAMPLEZ_LIBM: generic path
         SampleZOut o = sample_z(mu, s, a.precision, a.linear_probs != 0,
                                 rs.u((uint32_t)(a.d - 1 - i)), WL, a.etab, CERT ? dmu : -1.0);
         amb = CERT && o.z == kAmbZ;
@@ -836,7 +838,7 @@ __device__ unsigned long long lgs_diag_cycles[16];
 #endif
 // OZ (32-row panels only): far field as an exact int8-digit product on
 // v_mfma_i32_16x16x64_i8 instead of fp64 MFMA (see oz_far_field).
-template <typename ZT, int PB, bool WL, bool OZ = false>
+template <typename ZT, int PB, bool WL, bool OZ = false, bool LIBM = false>
 __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 3) void klein_mfma_kernel(const KleinArgs a,
                                                             const double* __restrict__ RP,
                                                             const double* __restrict__ RC,
@@ -1054,7 +1056,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         // bounded by the cap a.z1cap, checked after the sub-panel); a
                         // decision not covered is a guess, verified after the sub-panel
                         bool un;
-                        const double zi = decide_coord_rec<WL, true>(a, i, mu, rec, rs, lw, flags, etab_s,
+                        const double zi = decide_coord_rec<WL, true, LIBM>(a, i, mu, rec, rs, lw, flags, etab_s,
                                                                      cert_dmu(rec[kSzCa], rec[kSzCb], a.z1cap, mu),
                                                                      un);
                         if (un) cert_fl[threadIdx.x] |= 1 << s;
@@ -1845,12 +1847,21 @@ template <typename ZT, int PB>
 static void klein_pb(const KleinArgs& a, const double* RP, const double* RC, int kernel, bool wl,
                      ZT* z, dim3 grid, hipStream_t st) {
     if (kernel == kKernelMfma) {
+        const bool libm = a.szc == nullptr;
         if (PB == 32 && a.rd) {  // int8-digit far field
-            if (wl)
+            if (libm && wl)
+                hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, true, true, true>), grid, dim3(256), 0, st, a, RP, RC, z);
+            else if (libm)
+                hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, false, true, true>), grid, dim3(256), 0, st, a, RP, RC, z);
+            else if (wl)
                 hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, true, true>), grid, dim3(256), 0, st, a, RP, RC, z);
             else
                 hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, false, true>), grid, dim3(256), 0, st, a, RP, RC, z);
-        } else if (wl)
+        } else if (libm && wl)
+            hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, true, false, true>), grid, dim3(256), 0, st, a, RP, RC, z);
+        else if (libm)
+            hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, false, false, true>), grid, dim3(256), 0, st, a, RP, RC, z);
+        else if (wl)
             hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, true>), grid, dim3(256), 0, st, a, RP, RC, z);
         else
             hipLaunchKernelGGL((klein_mfma_kernel<ZT, PB, false>), grid, dim3(256), 0, st, a, RP, RC, z);
