@@ -746,29 +746,28 @@ __device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qi
         // than 2^-60 of the mass (q[7], host); otherwise such a point only matters for
         // u < 2^-60, i.e. u = 0.  Not covered: the decision as a guess, log_norm = NaN
         const bool doubt = cert && (q[7] != 0.0 ? !ends_stable(mu, q[6], dmu) : u == 0.0);
-        if (hi - lo == 1.0) {
-            // two points whose weights differ by more than e^745.2: the smaller
-            // one is exactly 0 in fp64 (as in the general loop below), so the
-            // decision is the heavier point for every u -- certified when the gap
-            // (moving at 1/s^2 per unit of mean) stays above 745.2 within dmu
-            const double t0 = (lo - mu) * is, t1 = (hi - mu) * is;
-            const double e0 = -0.5 * (t0 * t0), e1 = -0.5 * (t1 * t1);
-            const double em = fmax(e0, e1);
-            const double gap = em - fmin(e0, e1);
-            if (gap > 745.2 && !(linear_probs && em < -745.2)) {
-                log_norm = (doubt || (cert && !(gap - 745.2 > 1.01 * dmu * (is * is) + 1e-12 * gap)))
-                               ? __builtin_nan("")
-                               : (want_log ? em : 0.0);
-                return e0 > e1 ? lo : hi;
-            }
-        }
         double e[4];
-        double emax = -INFINITY;
+        double emax = -INFINITY, e2 = -INFINITY, kmax = lo;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const double t = ((lo + (double)k) - mu) * is;
             e[k] = lo + (double)k <= hi ? -0.5 * (t * t) : -INFINITY;
-            emax = fmax(emax, e[k]);
+            const bool top = e[k] > emax;
+            e2 = top ? emax : fmax(e2, e[k]);
+            kmax = top ? lo + (double)k : kmax;
+            emax = top ? e[k] : emax;
+        }
+        // one point outweighs every other by more than e^745.2: the others are
+        // exactly 0 in fp64 (as in the general loop below), so the decision is that
+        // point for every u (NTRU's sigma_i ~ 1e-3 coordinates, 2- and 3-point
+        // windows) -- certified when the gap, moving by at most (hi - lo) / s^2 per
+        // unit of mean, stays above 745.2 within dmu
+        const double gap = emax - e2;
+        if (gap > 745.2 && !(linear_probs && emax < -745.2)) {
+            log_norm = (doubt || (cert && !(gap - 745.2 > 1.01 * dmu * (hi - lo) * (is * is) + 1e-12 * gap)))
+                           ? __builtin_nan("")
+                           : (want_log ? emax : 0.0);
+            return kmax;
         }
         if (linear_probs && emax < -745.2) {
             log_norm = cert ? __builtin_nan("") : -INFINITY;
