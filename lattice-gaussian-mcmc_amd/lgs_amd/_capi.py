@@ -130,6 +130,8 @@ def _ptr(a):
             raise ValueError("arrays must be C-contiguous")
         return ctypes.c_void_p(a.ctypes.data)
     if hasattr(a, "data_ptr"):
+        if hasattr(a, "is_contiguous") and not a.is_contiguous():
+            raise ValueError("tensors must be contiguous")
         return ctypes.c_void_p(a.data_ptr())
     if isinstance(a, int):
         return ctypes.c_void_p(a)
@@ -138,6 +140,25 @@ def _ptr(a):
 
 def _dtype_name(a):
     return str(a.dtype).replace("torch.", "")
+
+
+def _check_bufs(flags, device, bufs):
+    """Caller buffers must match the call's flags: element type (LGS_Z64 selects
+    int64 coefficients), and host vs device memory (LGS_DEVICE_PTRS, on the
+    context's device) -- a mismatch would be silently misread by the library."""
+    dev_flag = bool(flags & LGS_DEVICE_PTRS)
+    for a, want, name in bufs:
+        if a is None:
+            continue
+        got = _dtype_name(a)
+        if got != want:
+            raise ValueError(f"{name}: expected {want}, got {got}")
+        is_dev = bool(getattr(a, "is_cuda", False))
+        if is_dev != dev_flag:
+            raise ValueError(f"{name}: {'device' if is_dev else 'host'} buffer with LGS_DEVICE_PTRS "
+                             f"{'set' if dev_flag else 'unset'}")
+        if is_dev and a.device.index is not None and a.device.index != device:
+            raise ValueError(f"{name}: on cuda:{a.device.index}, context on cuda:{device}")
 
 
 def x_flags(a) -> int:
@@ -192,6 +213,9 @@ class Context:
     # ---------------------------------------------------------------- compute
     def klein(self, seed, first, n, z_out=None, v_out=None, logw_out=None, flags=0):
         """Raw lgs_klein on caller-provided buffers (numpy host or device tensors)."""
+        zt = "int64" if flags & LGS_Z64 else "int32"
+        _check_bufs(flags, self.device, ((z_out, zt, "z_out"), (v_out, "float64", "v_out"),
+                                         (logw_out, "float64", "logw_out")))
         _check(_lib.lgs_klein(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(first), int(n),
                               _ptr(z_out), _ptr(v_out), _ptr(logw_out), int(flags)))
 
@@ -214,6 +238,11 @@ class Context:
 
     def imhk(self, seed, first_chain, n_chains, first_step, n_steps, thin, z_state, logw_state,
              state_init, accepts, z_samples=None, v_samples=None, moments=None, flags=0):
+        zt = "int64" if flags & LGS_Z64 else "int32"
+        _check_bufs(flags, self.device, ((z_state, zt, "z_state"), (logw_state, "float64", "logw_state"),
+                                         (state_init, "int32", "state_init"), (accepts, "int64", "accepts"),
+                                         (z_samples, zt, "z_samples"), (v_samples, "float64", "v_samples"),
+                                         (moments, "int64", "moments")))
         _check(_lib.lgs_imhk(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(first_chain),
                              int(n_chains), int(first_step), int(n_steps), int(thin),
                              _ptr(z_state), _ptr(logw_state), _ptr(state_init), _ptr(accepts),

@@ -39,6 +39,10 @@ def golden_R(g):
     import lgs_oracle
     B = lattices.ntru_basis(int(g["ntru_n"]), int(g["ntru_q"]), int(g["ntru_seed"]))
     R, cp = lgs_oracle.qr_prepare(B)
+    if "R_sha256" in g:  # the golden's input must be the reference's R bit for bit
+        import hashlib
+        got = hashlib.sha256(np.ascontiguousarray(R).tobytes()).hexdigest()
+        assert got == str(g["R_sha256"]), "rebuilt R differs from the reference's (LAPACK build?)"
     return R, cp, B
 
 

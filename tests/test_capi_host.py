@@ -141,3 +141,18 @@ def test_io_formats_match_reference_schema(tmp_path):
     back = io.load_samples_npz(str(tmp_path / "s.npz"))
     assert np.array_equal(back["samples"], s)
     np.testing.assert_allclose(back["norms"], np.linalg.norm(s, axis=1))
+
+
+def test_buffer_checks_reject_mismatched_dtype_and_memory():
+    """a buffer whose dtype or memory space disagrees with the call's
+    flags is rejected before it reaches the C-ABI (it would be misread)."""
+    import torch
+    from lgs_amd import _capi
+    ok32 = np.zeros((4, 3), dtype=np.int32)
+    _capi._check_bufs(0, 0, ((ok32, "int32", "z"),))
+    with pytest.raises(ValueError, match="expected int64"):
+        _capi._check_bufs(_capi.LGS_Z64, 0, ((ok32, "int64", "z"),))
+    with pytest.raises(ValueError, match="host buffer"):
+        _capi._check_bufs(_capi.LGS_DEVICE_PTRS, 0, ((torch.zeros(3, dtype=torch.float64), "float64", "v"),))
+    with pytest.raises(ValueError, match="contiguous"):
+        _capi._ptr(torch.zeros((4, 4))[:, 1])

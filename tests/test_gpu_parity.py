@@ -398,6 +398,17 @@ def test_samplez_reference_decision_table(ctx, table):
     assert np.array_equal(z, g["z"])
 
 
+def test_samplez_log_normalisers_vs_reference(ctx):
+    """Device 1-D normalisers (the Wang-Ling weight's factors) vs
+    the reference's own window logsumexp (tests/golden/samplez_lognorm.npz), on the
+    Euler-Maclaurin path and the table walk."""
+    g = load_golden("samplez_lognorm.npz")
+    u = np.full(g["mu"].size, 0.5)
+    for table in (False, True):
+        _, ln = ctx.sample_z(g["mu"], g["sigma"], u, table=table)
+        np.testing.assert_allclose(ln, g["log_norm"], rtol=1e-12, atol=1e-12)
+
+
 def _window(mu, sig, precision=10):
     rf = np.where(sig < 0.1, max(precision, 3), precision).astype(np.float64)
     lo = np.floor(mu - rf * sig).astype(np.int64)

@@ -154,3 +154,20 @@ def test_numpy_restatement_matches_oracle(oracle):
         v = nk.sample_single(lambda slot, c=c: oracle.philox_u(seed, slot, 0, c, 0))
         o = oracle.klein(R, cp, 3.0, 1, seed=seed, first_sample=c, B=B)
         np.testing.assert_array_equal(v, o["v"][0])
+
+
+def test_window_normalisers_vs_reference(oracle):
+    """log rho_sigma(window - mu) of the reference's own _compute_1d_probabilities
+    (klein.py:113-134; tests/golden/samplez_lognorm.npz) -- the building block of the
+    Wang-Ling weight and delta -- against the oracle's scipy-order
+    logsumexp over the same support.  The fixture also records that the reference's
+    Jacobi theta (utils.py:141-206) returns 0 for these arguments."""
+    g = load_golden("samplez_lognorm.npz")
+    for i in range(0, g["mu"].size, 7):
+        lo, npts = oracle.support(float(g["mu"][i]), float(g["sigma"][i]))
+        hi = lo + npts - 1
+        assert (lo, hi) == (int(g["lo"][i]), int(g["hi"][i]))
+        k = np.arange(lo, hi + 1)
+        raw = -0.5 * ((k - g["mu"][i]) / g["sigma"][i]) ** 2
+        assert abs(oracle.logsumexp(raw) - g["log_norm"][i]) <= 1e-13 * max(1.0, abs(g["log_norm"][i]))
+    assert np.all(g["theta3_probe"] == 0)
