@@ -743,9 +743,11 @@ __device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qi
         const double is = q[1];
         constexpr bool cert = CERT;
         // window ends: checked when the points they can add or drop may carry more
-        // than 2^-60 of the mass (q[7], host); otherwise such a point only matters for
-        // u < 2^-60, i.e. u = 0.  Not covered: the decision as a guess, log_norm = NaN
-        const bool doubt = cert && (q[7] != 0.0 ? !ends_stable(mu, q[6], dmu) : u == 0.0);
+        // than 2^-60 of the mass (q[7] = 1, host); below that such a point only
+        // matters for u < 2^-60, i.e. u = 0 (q[7] = 0.5), and not at all when its
+        // probability is exactly 0 (q[7] = 0).  Not covered: the decision as a
+        // guess, log_norm = NaN
+        const bool doubt = cert && (q[7] == 1.0 ? !ends_stable(mu, q[6], dmu) : (q[7] != 0.0 && u == 0.0));
         double e[4];
         double emax = -INFINITY, e2 = -INFINITY, kmax = lo;
 #pragma unroll

@@ -140,9 +140,36 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         zi = amb ? rint(mu) : (double)o.z;
         if (WL) lw += amb ? 0.0 : o.log_norm;
     } else {
-        double ln;
-        zi = sample_z_coord_t<CERT>(mu, rs.u((uint32_t)(a.d - 1 - i)), rec, a.precision,
-                                    a.linear_probs != 0, WL, etab, ln, dmu, amb);
+        // Inline one-dominant-point decision of the small kind (NTRU's sigma_i ~ 1e-3
+        // coordinates), certified as in sample_z_coord_body: no call and no Philox
+        // draw (the counter-addressed uniform is simply not generated: its value
+        // cannot matter when every other window point, and any point the window's
+        // ends could add, has probability exactly 0 -- rec[7] == 0)
+        bool fast = false;
+        double ln = 0.0;
+        if (CERT && (int)rec[2] == kSzSmall && rec[7] == 0.0) {
+            const double lo = floor(mu - rec[6]), hi = ceil(mu + rec[6]), is = rec[1];
+            if (hi - lo <= 3.0) {
+                double emax = -INFINITY, e2 = -INFINITY, kmax = lo;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const double t = ((lo + (double)k) - mu) * is;
+                    const double e = lo + (double)k <= hi ? -0.5 * (t * t) : -INFINITY;
+                    const bool top = e > emax;
+                    e2 = top ? emax : fmax(e2, e);
+                    kmax = top ? lo + (double)k : kmax;
+                    emax = top ? e : emax;
+                }
+                const double gap = emax - e2;
+                fast = gap > 745.2 && !(a.linear_probs && emax < -745.2) &&
+                       gap - 745.2 > 1.01 * dmu * (hi - lo) * (is * is) + 1e-12 * gap;
+                zi = kmax;
+                ln = emax;
+            }
+        }
+        if (!fast)
+            zi = sample_z_coord_t<CERT>(mu, rs.u((uint32_t)(a.d - 1 - i)), rec, a.precision,
+                                        a.linear_probs != 0, WL, etab, ln, dmu, amb);
         if (WL) lw += ln;
     }
     if (!WL) {

@@ -63,8 +63,10 @@ inline void build_szc(double s, int precision, double* q) {
         q[2] = lgs::kSzSmall;
         // a point entering / leaving at a window end lies >= q6 + 1 from mu while a
         // window point lies within 1/2: relative mass <= exp(-((q6+1)^2 - 1/4) / (2 s^2))
+        // q[7]: 0 -- such a point's probability is exactly 0 in fp64 (e^-746); 0.5 --
+        // below 2^-60 = e^-41.6 (matters only for u = 0); 1 -- the ends are checked
         const double e = ((q[6] + 1.0) * (q[6] + 1.0) - 0.25) / (2.0 * s * s);
-        q[7] = e > 42.0 ? 0.0 : 1.0;  // 2^-60 = e^-41.6
+        q[7] = e > 746.0 ? 0.0 : (e > 42.0 ? 0.5 : 1.0);
         return;
     }
     const double W = 2.0 * q[6];
