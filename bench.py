@@ -137,35 +137,37 @@ def load_counters(path, config):
 class LagSums:
     """Lag-L autocovariance sums of per-chain scalar series, continued across bench
     steps through a ring of each chain's last L values.  int64 sums
-    (exact, order-independent) for integer series, fp64 otherwise."""
+    (exact, order-independent) for integer series, fp64 otherwise.  One update is a
+    handful of device kernels: the ring starts as zeros, so pairs reaching before
+    the first step contribute nothing and only the pair counts (host integers)
+    need the history length."""
 
     def __init__(self, torch, n_chains, L, dtype, device):
         self.t, self.L = torch, L
         self.ring = torch.zeros((n_chains, L), dtype=dtype, device=device)
         self.have = 0
         self.S = torch.zeros(L + 1, dtype=dtype, device=device)   # sum_t x_t x_{t-k}
-        self.N = torch.zeros(L + 1, dtype=torch.int64, device=device)  # pairs per lag
+        self.N = np.zeros(L + 1, dtype=np.int64)                  # pairs per lag
         self.S1 = torch.zeros(1, dtype=dtype, device=device)
-        self.n = torch.zeros(1, dtype=torch.int64, device=device)
+        self.n = 0
 
     def update(self, x):
         torch, L, h = self.t, self.L, self.have
         nc, T = x.shape
-        xs = torch.cat([self.ring[:, L - h:], x], 1)
-        for k in range(L + 1):
-            t0 = max(0, k - h)
-            if t0 >= T:
-                continue
-            self.S[k] += (x[:, t0:] * xs[:, h + t0 - k:h + T - k]).sum()
-            self.N[k] += nc * (T - t0)
+        xs = torch.cat([self.ring, x], 1)                      # (nc, L + T)
+        win = xs.unfold(1, T, 1).flip(1)                       # win[:, k] = xs[:, L - k : L - k + T]
+        self.S += (win * x[:, None, :]).sum((0, 2))
+        k = np.arange(L + 1)
+        self.N += nc * np.maximum(T - np.maximum(k - h, 0), 0)
         self.S1 += x.sum()
         self.n += x.numel()
-        keep = min(L, h + T)
-        self.ring[:, L - keep:] = xs[:, xs.shape[1] - keep:]
-        self.have = keep
+        self.ring = xs[:, T:].clone() if T < L else x[:, T - L:].clone()
+        self.have = min(L, h + T)
 
     def parts(self):
-        return [self.S, self.N, self.S1, self.n]
+        t = self.t
+        dev = self.S.device
+        return [self.S, t.from_numpy(self.N).to(dev), self.S1, t.tensor([self.n], dtype=t.int64, device=dev)]
 
     @staticmethod
     def acf(S, N, S1, n):
