@@ -337,13 +337,28 @@ __device__ __forceinline__ double mu_exact_wave(const double* __restrict__ R, co
 // with bit 16) the whole sub-panel is replayed in the reference's order from the
 // weight and |z| sum of its start, rewriting L's coefficients and (OZ) history.
 // The decisions of lane L are computed redundantly by every lane (uniform inputs).
-// Returns the calling lane's weight; updates its |z| sum (z1l[lane]) and flags.
+// Returns the calling lane's weight, flags and nonzero bit (in registers: an output
+// through a reference would keep the caller's copy in scratch memory, with a
+// load-and-wait at every use); updates its |z| sum (z1l[lane]).
+// A: the launch's arguments where the kernel received them (the kernarg segment,
+// constant address space: scalar loads).  Taking the address of the by-value
+// kernel argument instead makes the compiler copy the whole struct to scratch and
+// read every field of it from there in the hot loop.
+using KArgsPtr = const __attribute__((address_space(4))) KleinArgs*;
+__device__ __forceinline__ KArgsPtr kernel_args() {
+    return (KArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();  // KleinArgs is argument 0: offset 0
+}
+struct VerifyOut {
+    double lw;
+    unsigned int flags;
+    int nz;
+};
 template <bool WL, bool OZ, typename ZT>
-__device__ __noinline__ double verify_subpanel(const KleinArgs* __restrict__ A, ZT* __restrict__ Z, size_t ldz,
-                                               int64_t p0, int top, int rows, int fl, double lw,
-                                               uint32_t step, uint32_t chain, double* z1l,
-                                               const double* z1s, const double* lws, unsigned int& flags,
-                                               int& nz) {
+__device__ __noinline__ VerifyOut verify_subpanel(KArgsPtr A, ZT* __restrict__ Z, size_t ldz,
+                                                  int64_t p0, int top, int rows, int fl, double lw,
+                                                  uint32_t step, uint32_t chain, double* z1l,
+                                                  const double* z1s, const double* lws, unsigned int flags) {
+    int nz = 0;
     const int lane = threadIdx.x & 63;
     const int d = A->d;
     // the sub-panel's coefficients / history were just stored by their own lanes and
@@ -441,7 +456,7 @@ __device__ __noinline__ double verify_subpanel(const KleinArgs* __restrict__ A, 
         }
         if (lane == 0) atomicAdd(A->flags + kFlagWordResolved, 1u);
     }
-    return lw;
+    return VerifyOut{lw, flags, nz};
 }
 
 // ------------------------------------------------------------ exact order
@@ -1163,11 +1178,12 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                 if (__builtin_amdgcn_ballot_w64(fl != 0) != 0) {  // rare: verify / replay (whole wave)
                     cert_fl[threadIdx.x] = 0;
                     const int w64 = threadIdx.x & ~63;
-                    int nzv = 0;
-                    lw = verify_subpanel<WL, OZ>(&a, Z, ldz, p0, top, rows16, fl, lw, rs.step, rs.chain,
-                                                 &cert_lds[0][w64], &cert_lds[1][w64], &cert_lds[2][w64],
-                                                 flags, nzv);
-                    if constexpr (OZ) pnz |= nzv != 0;
+                    const VerifyOut vo = verify_subpanel<WL, OZ>(kernel_args(), Z, ldz, p0, top, rows16, fl, lw,
+                                                                 rs.step, rs.chain, &cert_lds[0][w64],
+                                                                 &cert_lds[1][w64], &cert_lds[2][w64], flags);
+                    lw = vo.lw;
+                    flags = vo.flags;
+                    if constexpr (OZ) pnz |= vo.nz != 0;
                 }
             };
             near16(p_hi < 16 ? p_hi : 16, p_hi);
