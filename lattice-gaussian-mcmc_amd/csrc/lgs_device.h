@@ -396,6 +396,57 @@ __device__ __forceinline__ ErfExp erf_gauss(double y, CoefTab tab) {
     return r;
 }
 
+// Series form for |y| <= 1 (capped windows with sigma >= 360: |k - mu| <= 500.5
+// gives |y| <= 0.983): erf(y) = 2/sqrt(pi) sum_{n<=17} (-1)^n y^(2n+1)/(n! (2n+1))
+// and e^{-y^2} = sum_{n<=18} (-y^2)^n/n!, truncation < 5e-18 and < 1e-17, within
+// 3e-16 / 5e-16 relative of libm over [0, 1] -- no table lookup (a gather whose
+// latency sits on the decision's dependency chain), two independent Horner chains.
+struct PolyErf {};
+__device__ __forceinline__ ErfExp erf_gauss(double y, PolyErf) {
+    const double z = y * y;
+    double e = -9.063970842808673e-17;
+    e = fma(e, z, 1.6342614095367152e-15);
+    e = fma(e, z, -2.7835162072109215e-14);
+    e = fma(e, z, 4.4632242632864775e-13);
+    e = fma(e, z, -6.7113668551641105e-12);
+    e = fma(e, z, 9.422759064650411e-11);
+    e = fma(e, z, -1.2290555301717928e-09);
+    e = fma(e, z, 1.4807192815879218e-08);
+    e = fma(e, z, -1.6365844691234924e-07);
+    e = fma(e, z, 1.6462114365889248e-06);
+    e = fma(e, z, -1.492565035840625e-05);
+    e = fma(e, z, 0.00012055332981789664);
+    e = fma(e, z, -0.0008548327023450853);
+    e = fma(e, z, 0.005223977625442188);
+    e = fma(e, z, -0.026866170645131252);
+    e = fma(e, z, 0.11283791670955126);
+    e = fma(e, z, -0.37612638903183754);
+    e = fma(e, z, 1.1283791670955126);
+    double g = 1.5619206968586225e-16;
+    g = fma(g, z, -2.8114572543455206e-15);
+    g = fma(g, z, 4.779477332387385e-14);
+    g = fma(g, z, -7.647163731819816e-13);
+    g = fma(g, z, 1.1470745597729725e-11);
+    g = fma(g, z, -1.6059043836821613e-10);
+    g = fma(g, z, 2.08767569878681e-09);
+    g = fma(g, z, -2.505210838544172e-08);
+    g = fma(g, z, 2.755731922398589e-07);
+    g = fma(g, z, -2.7557319223985893e-06);
+    g = fma(g, z, 2.48015873015873e-05);
+    g = fma(g, z, -0.0001984126984126984);
+    g = fma(g, z, 0.001388888888888889);
+    g = fma(g, z, -0.008333333333333333);
+    g = fma(g, z, 0.041666666666666664);
+    g = fma(g, z, -0.16666666666666666);
+    g = fma(g, z, 0.5);
+    g = fma(g, z, -1.0);
+    g = fma(g, z, 1.0);
+    ErfExp r;
+    r.erf = y * e;
+    r.g = g;
+    return r;
+}
+
 // P(x) of the Euler-Maclaurin formula with NT Hermite correction terms
 // (NT = 6 for sigma < 50; 3 suffice above: the next term is < 1e-18 S).
 #define LGS_EM_ATTR __device__ __forceinline__
@@ -626,11 +677,38 @@ __device__ __forceinline__ double em_C_rel(double kd, double m, double sig, doub
     return em_P_tab<NT>(kd, m, sig, is, etab, fk) + 0.5 * fk - base;
 }
 
+// q[0..8] of a coordinate, loaded as one batch before any branch on them: one
+// memory round trip instead of one per branch level (the kind, then the window, ...)
+struct QHead {
+    double v[9];
+};
+template <typename QP>
+__device__ __forceinline__ QHead load_head(QP q) {
+    QHead h;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) h.v[k] = q[k];
+    return h;
+}
+// LDS records (16-byte aligned, klein_mfma_kernel rec_lds): four 16-byte reads + one
+__device__ __forceinline__ QHead load_head(lds_cdptr q) {
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    using lds_d2p = const __attribute__((address_space(3))) d2v*;
+    QHead h;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const d2v t = ((lds_d2p)q)[k];
+        h.v[2 * k] = t[0];
+        h.v[2 * k + 1] = t[1];
+    }
+    h.v[8] = q[8];
+    return h;
+}
+
 template <int NT, bool CERT, typename TP, typename QP>
-__device__ __forceinline__ double sample_z_wide(double mu, double u, QP q,
+__device__ __forceinline__ double sample_z_wide(double mu, double u, const QHead& h, QP q,
                                                 int kind, int precision, bool linear_probs,
                                                 bool want_log, TP etab, double& log_norm, double dmu) {
-    const double sig = q[0], is = q[1];
+    const double sig = h.v[0], is = h.v[1];
     const double c = rint(mu);
     const double m = mu - c;
     double S, base, a, b;
@@ -645,15 +723,15 @@ __device__ __forceinline__ double sample_z_wide(double mu, double u, QP q,
         a = -500.0;
         b = 500.0;
     } else {
-        S = q[7];
-        base = q[8];
-        a = floor(mu - q[6]) - c;
-        b = ceil(mu + q[6]) - c;
+        S = h.v[7];
+        base = h.v[8];
+        a = floor(mu - h.v[6]) - c;
+        b = ceil(mu + h.v[6]) - c;
     }
     const double target = u * S;
-    const float arg = fminf(fmaxf((float)((target + base) * q[4]), -1.0f + 0x1p-24f),
+    const float arg = fminf(fmaxf((float)((target + base) * h.v[4]), -1.0f + 0x1p-24f),
                             1.0f - 0x1p-24f);
-    const float xg = fmaf((float)q[5], erfinvf(arg), (float)m);
+    const float xg = fmaf((float)h.v[5], erfinvf(arg), (float)m);
     double kd = fmin(fmax((double)ceilf(xg - 0.5f), a), b);
     double fk;
     double Ck = em_C_rel<NT>(kd, m, sig, is, etab, base, fk);
@@ -734,20 +812,22 @@ __device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qi
                                                       bool linear_probs, bool want_log, TP etab,
                                                       double& log_norm, double dmu) {
     const QP q = uniformize(qin);  // all lanes are on the same coordinate
-    const int kind = (int)q[2];
-    const double sig = q[0];
+    const QHead qh = load_head(q);
+    const int kind = (int)qh.v[2];
+    const double sig = qh.v[0];
     if (kind == kSzSmall) {
-        const double lo = floor(mu - q[6]);
-        const double hi = ceil(mu + q[6]);
+        const double lo = floor(mu - qh.v[6]);
+        const double hi = ceil(mu + qh.v[6]);
         if (hi - lo > 3.0) return __builtin_nan("");
-        const double is = q[1];
+        const double is = qh.v[1];
         constexpr bool cert = CERT;
         // window ends: checked when the points they can add or drop may carry more
         // than 2^-60 of the mass (q[7] = 1, host); below that such a point only
         // matters for u < 2^-60, i.e. u = 0 (q[7] = 0.5), and not at all when its
         // probability is exactly 0 (q[7] = 0).  Not covered: the decision as a
         // guess, log_norm = NaN
-        const bool doubt = cert && (q[7] == 1.0 ? !ends_stable(mu, q[6], dmu) : (q[7] != 0.0 && u == 0.0));
+        const bool doubt =
+            cert && (qh.v[7] == 1.0 ? !ends_stable(mu, qh.v[6], dmu) : (qh.v[7] != 0.0 && u == 0.0));
         double e[4];
         double emax = -INFINITY, e2 = -INFINITY, kmax = lo;
 #pragma unroll
@@ -808,9 +888,14 @@ __device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qi
         return z;
     }
     if (kind == kSzGeneric) return __builtin_nan("");
+#ifndef LGS_NO_CAPPED_POLY
+    if (kind == kSzCapped && qh.v[7] == 1.0)  // sigma >= 360 (host): series erf / exp
+        return sample_z_wide<3, CERT>(mu, u, qh, q, kind, precision, linear_probs, want_log, PolyErf{},
+                                      log_norm, dmu);
+#endif
     return sig < 50.0
-               ? sample_z_wide<6, CERT>(mu, u, q, kind, precision, linear_probs, want_log, etab, log_norm, dmu)
-               : sample_z_wide<3, CERT>(mu, u, q, kind, precision, linear_probs, want_log, etab, log_norm, dmu);
+               ? sample_z_wide<6, CERT>(mu, u, qh, q, kind, precision, linear_probs, want_log, etab, log_norm, dmu)
+               : sample_z_wide<3, CERT>(mu, u, qh, q, kind, precision, linear_probs, want_log, etab, log_norm, dmu);
 }
 
 // Both results come back in registers (a reference parameter of a call lives in

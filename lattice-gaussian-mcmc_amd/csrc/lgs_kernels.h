@@ -21,7 +21,8 @@ constexpr int kCoefStride = 18;  // doubles per grid point of the coefficient ta
 // the host in lgs_set_basis; lgs_device.h sample_z_coord):
 //   [0] sigma_i  [1] 1/sigma_i  [2] kind  [3] sc = sigma*sqrt(pi/2)  [4] 1/sc
 //   [5] sigma*sqrt(2)  [6] rf*sigma (window half-width, klein.py:113-120)
-//   [7] S, [8] base (kind kSzClosed)
+//   [7] S, [8] base (kind kSzClosed); [7] of the capped kind: 1 when sigma >= 360
+//   (series erf / exp over the whole window, lgs_device.h PolyErf)
 //   [kSzS..kSzS+kSzDeg] / [kSzB..kSzB+kSzDeg]: monomial coefficients in
 //   m = mu - rint(mu) of S(m) / base(m) (kind kSzCapped)
 //   [kSzCa], [kSzCb]: decision certificate of the blocked kernels (lgs_device.h

@@ -115,7 +115,8 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         flags |= kFlagNonFinite;
         return 0.0;
     }
-    const double s = rec[0];
+    const QHead qh = load_head(rec);  // the fields branched on below, in one LDS round trip
+    const double s = qh.v[0];
 #ifdef LGS_DIAG_NO_SAMPLEZ
     if (true) {
         zi = rint(mu + rs.u((uint32_t)(a.d - 1 - i)) * 1e-300);
@@ -147,8 +148,8 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         // ends could add, has probability exactly 0 -- rec[7] == 0)
         bool fast = false;
         double ln = 0.0;
-        if (CERT && (int)rec[2] == kSzSmall && rec[7] == 0.0) {
-            const double lo = floor(mu - rec[6]), hi = ceil(mu + rec[6]), is = rec[1];
+        if (CERT && (int)qh.v[2] == kSzSmall && qh.v[7] == 0.0) {
+            const double lo = floor(mu - qh.v[6]), hi = ceil(mu + qh.v[6]), is = qh.v[1];
             if (hi - lo <= 3.0) {
                 double emax = -INFINITY, e2 = -INFINITY, kmax = lo;
 #pragma unroll
@@ -907,7 +908,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
         etab_s = stage_etab(tab_lds, a.etab);
 #endif
     // 32-row panels: the panel's per-coordinate records, staged block-wide
-    __shared__ double rec_lds[PB == 32 ? 32 * kRecStride : 2];
+    __shared__ __attribute__((aligned(16))) double rec_lds[PB == 32 ? 32 * kRecStride : 2];
     // OZ: bit q set when panel q has a nonzero coefficient in some sample of the block
     __shared__ uint32_t nzm[OZ ? kOzMaxD / 32 / 32 : 1];
     if constexpr (OZ)
@@ -1092,14 +1093,20 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         // running sums rotate instead of shifting: logical acc[k] of step s
                         // lives in acc[(k - s) & 15] (s is a compile-time constant here), so
                         // no register moves per coordinate; 16 steps bring the map back
-                        const double mu = (rec[kRecCp] - acc[(15 - s) & 15]) * rec[kRecIrii];
+                        // Ca, Cb, c', 1/R_ii (record slots 21..24) in two 16-byte LDS reads
+                        static_assert(kSzCa == 21 && kSzCb == 22 && kRecCp == 23 && kRecIrii == 24, "record layout");
+                        typedef double d2v __attribute__((ext_vector_type(2)));
+                        const d2v r22 = ((const __attribute__((address_space(3))) d2v*)rec)[11];
+                        const d2v r24 = ((const __attribute__((address_space(3))) d2v*)rec)[12];
+                        const double rca = rec[kSzCa];
+                        const double mu = (r22[1] - acc[(15 - s) & 15]) * r24[0];
                         LGS_DC_T(t_sz0);
                         // certified decision at the blocked-order mean (the |z| sum
                         // bounded by the cap a.z1cap, checked after the sub-panel); a
                         // decision not covered is a guess, verified after the sub-panel
                         bool un;
                         const double zi = decide_coord_rec<WL, true, LIBM>(a, i, mu, rec, rs, lw, flags, etab_s,
-                                                                     cert_dmu(rec[kSzCa], rec[kSzCb], a.z1cap, mu),
+                                                                     cert_dmu(rca, r22[0], a.z1cap, mu),
                                                                      un);
                         if (un) cert_fl[threadIdx.x] |= 1 << s;
 #ifdef LGS_DIAG_CYCLES

@@ -130,7 +130,12 @@ inline void build_szc(double s, int precision, double* q) {
         err = std::max(err, std::max(fabsl((long double)S - Se), fabsl((long double)b - be)));
         Smin = std::min(Smin, Se);
     }
-    if (err <= 5e-16L * Smin) q[2] = lgs::kSzCapped;  // ~2 ulp of S
+    if (err <= 5e-16L * Smin) {  // ~2 ulp of S
+        q[2] = lgs::kSzCapped;
+        // |k - mu| <= 500.5 in the window: |k - mu| / (sigma sqrt 2) <= 1 from sigma >=
+        // 354, the range of the series erf / exp (lgs_device.h PolyErf)
+        q[7] = s >= 360.0 ? 1.0 : 0.0;
+    }
 }
 
 }  // namespace lgs_host
