@@ -43,6 +43,9 @@ __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
         k0 = __builtin_amdgcn_readfirstlane(k0);
         k1 = __builtin_amdgcn_readfirstlane(k1);
         asm volatile("" : "+s"(k0), "+s"(k1));
+        // likewise the first round's products of the per-lane (step, chain) words:
+        // hoisted, they were spilled and reloaded from scratch at every draw
+        asm volatile("" : "+v"(c1), "+v"(c2));
     }
 #endif
 #pragma unroll
@@ -767,6 +770,74 @@ __device__ __forceinline__ double sample_z_wide(double mu, double u, const QHead
     return c + kd;
 }
 
+// The capped kind with sigma >= 360 (q[7] == 1: NTRU / q-ary bases' large-sigma
+// coordinates), streamlined for latency -- the Klein kernels' per-coordinate
+// dependency chain runs through it: the quantile guess from a fixed fp64 erfinv
+// polynomial (|v| <= 0.849, relative error 3e-8; no branches, unlike erfinvf),
+// the series erf / exp (PolyErf), and the +-1 walk only behind a wave-uniform test
+// (the guess is off by one for ~4e-5 of the lanes).  Same decision rule, margins
+// and certificate as sample_z_wide.
+template <bool CERT, typename QP>
+__device__ __forceinline__ double sample_z_capped(double mu, double u, const QHead& h, QP q, bool want_log,
+                                                  double& log_norm, double dmu) {
+    const double sig = h.v[0], is = h.v[1];
+    const double c = rint(mu);
+    const double m = mu - c;
+    double S = q[kSzS + kSzDeg], base = q[kSzB + kSzDeg];
+#pragma unroll
+    for (int k = kSzDeg - 1; k >= 0; --k) {
+        S = fma(S, m, q[kSzS + k]);
+        base = fma(base, m, q[kSzB + k]);
+    }
+    const double target = u * S;
+    // continuous quantile x = m + sigma sqrt(2) erfinv(v): erfinv(v) = v R(v^2)
+    const double v = fmin(fmax((target + base) * h.v[4], -0.8485), 0.8485);
+    const double w = v * v;
+    double r = 11.853485934431038;
+    r = fma(r, w, -43.593212219926436);
+    r = fma(r, w, 71.76515059941498);
+    r = fma(r, w, -68.64189227692192);
+    r = fma(r, w, 42.14891487326897);
+    r = fma(r, w, -17.187235185827564);
+    r = fma(r, w, 4.787814391235978);
+    r = fma(r, w, -0.8188084361376584);
+    r = fma(r, w, 0.16780265291085433);
+    r = fma(r, w, 0.07920907048159789);
+    r = fma(r, w, 0.1278390124627034);
+    r = fma(r, w, 0.23200895985592382);
+    r = fma(r, w, 0.8862269447150851);
+    const double xg = fma(h.v[5] * v, r, m);
+    double kd = fmin(fmax(ceil(xg - 0.5), -500.0), 500.0);
+    double fk;
+    double Ck = em_C_rel<3>(kd, m, sig, is, PolyErf{}, base, fk);
+    if (__builtin_amdgcn_ballot_w64(!(Ck > target) || (kd > -500.0 && Ck - fk > target)) != 0) {
+#pragma nounroll
+        for (int it = 0; it < 64 && Ck <= target && kd < 500.0; ++it) {  // move up
+            kd += 1.0;
+            fk = gauss_tab(kd, m, is, PolyErf{});
+            Ck += fk;
+        }
+#pragma nounroll
+        for (int it = 0; it < 64 && kd > -500.0 && Ck - fk > target; ++it) {  // move down
+            Ck -= fk;
+            kd -= 1.0;
+            fk = gauss_tab(kd, m, is, PolyErf{});
+        }
+    }
+    const double margin = fmin(Ck - target, kd > -500.0 ? target - (Ck - fk) : target);
+    if constexpr (CERT) {
+        if (!(Ck > target)) return __builtin_nan("");
+        if (!(margin > fma(0.6 * dmu, is, 1e-12) * S) || !(fabs(m) + 1.01 * dmu < 0.5)) {
+            log_norm = __builtin_nan("");
+            return c + kd;
+        }
+    } else if (!(margin > 1e-12 * S) || !(Ck > target)) {
+        return __builtin_nan("");
+    }
+    log_norm = want_log ? log(S) : 0.0;
+    return c + kd;
+}
+
 // Both window ends evaluated per draw (kinds without precomputed normalisers);
 // out of line: its two concurrent erf evaluations would otherwise set the
 // register footprint of sample_z_coord.
@@ -890,8 +961,7 @@ __device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qi
     if (kind == kSzGeneric) return __builtin_nan("");
 #ifndef LGS_NO_CAPPED_POLY
     if (kind == kSzCapped && qh.v[7] == 1.0)  // sigma >= 360 (host): series erf / exp
-        return sample_z_wide<3, CERT>(mu, u, qh, q, kind, precision, linear_probs, want_log, PolyErf{},
-                                      log_norm, dmu);
+        return sample_z_capped<CERT>(mu, u, qh, q, want_log, log_norm, dmu);
 #endif
     return sig < 50.0
                ? sample_z_wide<6, CERT>(mu, u, qh, q, kind, precision, linear_probs, want_log, etab, log_norm, dmu)
@@ -945,11 +1015,29 @@ __device__ __forceinline__ double sample_z_coord(double mu, double u, QP q, int 
 // The same with the certificate fixed at compile time (hot loops: one call target).
 // The same with the certificate fixed at compile time (hot loops: one call target);
 // CERT: always returns a decision (a guess when not covered: amb = true, log_norm = 0).
+// The capped kind with sigma >= 360 alone (klein_mfma_kernel dispatches on the
+// kind itself): a small leaf, no kind dispatch inside.
+template <bool CERT, typename QP>
+#ifdef LGS_CAPPED_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+SzPair sample_z_capped_leaf(double mu, double u, QP q, bool want_log, double dmu) {
+    const QP qu = uniformize(q);
+    const QHead qh = load_head(qu);
+    SzPair r;
+    r.ln = 0.0;
+    r.z = sample_z_capped<CERT>(mu, u, qh, qu, want_log, r.ln, dmu);
+    return r;
+}
+
+// The NaN conventions of a leaf's result resolved (fallback decision; CERT: guess
+// flagged in amb).
 template <bool CERT, typename TP, typename QP>
-__device__ __forceinline__ double sample_z_coord_t(double mu, double u, QP q, int precision,
-                                                   bool linear_probs, bool want_log, TP etab,
-                                                   double& log_norm, double dmu, bool& amb) {
-    const SzPair r = sample_z_coord_leaf<CERT>(mu, u, q, precision, linear_probs, want_log, etab, dmu);
+__device__ __forceinline__ double sz_finish(SzPair r, double mu, double u, QP q, int precision,
+                                            bool linear_probs, bool want_log, TP etab,
+                                            double& log_norm, double dmu, bool& amb) {
     double z = r.z;
     log_norm = r.ln;
     amb = false;
@@ -965,6 +1053,13 @@ __device__ __forceinline__ double sample_z_coord_t(double mu, double u, QP q, in
     }
     if (amb) log_norm = 0.0;
     return z;
+}
+template <bool CERT, typename TP, typename QP>
+__device__ __forceinline__ double sample_z_coord_t(double mu, double u, QP q, int precision,
+                                                   bool linear_probs, bool want_log, TP etab,
+                                                   double& log_norm, double dmu, bool& amb) {
+    const SzPair r = sample_z_coord_leaf<CERT>(mu, u, q, precision, linear_probs, want_log, etab, dmu);
+    return sz_finish<CERT>(r, mu, u, q, precision, linear_probs, want_log, etab, log_norm, dmu, amb);
 }
 
 // Conditional mean of coordinate i in the reference's order (klein.py:191-195:

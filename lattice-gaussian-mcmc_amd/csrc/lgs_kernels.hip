@@ -148,7 +148,10 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         // ends could add, has probability exactly 0 -- rec[7] == 0)
         bool fast = false;
         double ln = 0.0;
-        if (CERT && (int)qh.v[2] == kSzSmall && qh.v[7] == 0.0) {
+        // the kind and its flag are the same in every lane: scalar branches
+        const int kind = __builtin_amdgcn_readfirstlane((int)qh.v[2]);
+        const int q7 = __builtin_amdgcn_readfirstlane(qh.v[7] == 0.0 ? 0 : (qh.v[7] == 1.0 ? 1 : 2));
+        if (CERT && kind == kSzSmall && q7 == 0) {
             const double lo = floor(mu - qh.v[6]), hi = ceil(mu + qh.v[6]), is = qh.v[1];
             if (hi - lo <= 3.0) {
                 double emax = -INFINITY, e2 = -INFINITY, kmax = lo;
@@ -168,9 +171,17 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
                 ln = emax;
             }
         }
-        if (!fast)
-            zi = sample_z_coord_t<CERT>(mu, rs.u((uint32_t)(a.d - 1 - i)), rec, a.precision,
-                                        a.linear_probs != 0, WL, etab, ln, dmu, amb);
+        if (!fast) {
+            const double u = rs.u((uint32_t)(a.d - 1 - i));
+#ifndef LGS_NO_CAPPED_POLY
+            if (kind == kSzCapped && q7 == 1)  // sigma >= 360: the streamlined capped leaf
+                zi = sz_finish<CERT>(sample_z_capped_leaf<CERT>(mu, u, rec, WL, dmu), mu, u, rec, a.precision,
+                                     a.linear_probs != 0, WL, etab, ln, dmu, amb);
+            else
+#endif
+                zi = sample_z_coord_t<CERT>(mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, ln, dmu,
+                                            amb);
+        }
         if (WL) lw += ln;
     }
     if (!WL) {
