@@ -770,6 +770,55 @@ __device__ __forceinline__ double sample_z_wide(double mu, double u, const QHead
     return c + kd;
 }
 
+// Polynomial sum_k c[k] x^k by Estrin's scheme: depth ceil(log2 N) + 1 dependent
+// FMAs instead of Horner's N - 1 (the capped decision is latency-bound).
+template <int N>
+__device__ __forceinline__ double poly_estrin(const double (&c)[N], double x) {
+    double p[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) p[k] = c[k];
+    int n = N;
+    double xp = x;
+#pragma unroll
+    for (int lvl = 0; lvl < 6; ++lvl) {
+        if (n > 1) {
+#pragma unroll
+            for (int j = 0; j < (n + 1) / 2; ++j) p[j] = 2 * j + 1 < n ? fma(p[2 * j + 1], xp, p[2 * j]) : p[2 * j];
+            n = (n + 1) / 2;
+            xp = xp * xp;
+        }
+    }
+    return p[0];
+}
+
+// C(k) - base of a capped window with sigma >= 360 (Euler-Maclaurin with 3 terms,
+// as em_P_tab<3>), the series erf / exp in Estrin form; fk = f(k).
+__device__ __forceinline__ double capped_C(double kd, double m, double sig, double is, double base, double& fk) {
+    constexpr double E[18] = {1.1283791670955126, -0.37612638903183754, 0.11283791670955126,
+                              -0.026866170645131252, 0.005223977625442188, -0.0008548327023450853,
+                              0.00012055332981789664, -1.492565035840625e-05, 1.6462114365889248e-06,
+                              -1.6365844691234924e-07, 1.4807192815879218e-08, -1.2290555301717928e-09,
+                              9.422759064650411e-11, -6.7113668551641105e-12, 4.4632242632864775e-13,
+                              -2.7835162072109215e-14, 1.6342614095367152e-15, -9.063970842808673e-17};
+    constexpr double G[19] = {1.0, -1.0, 0.5, -0.16666666666666666, 0.041666666666666664,
+                              -0.008333333333333333, 0.001388888888888889, -0.0001984126984126984,
+                              2.48015873015873e-05, -2.7557319223985893e-06, 2.755731922398589e-07,
+                              -2.505210838544172e-08, 2.08767569878681e-09, -1.6059043836821613e-10,
+                              1.1470745597729725e-11, -7.647163731819816e-13, 4.779477332387385e-14,
+                              -2.8114572543455206e-15, 1.5619206968586225e-16};
+    const double t = (kd - m) * is;
+    const double t2 = t * t;
+    const double z = 0.5 * t2;  // y^2, y = t / sqrt 2
+    const double erf_y = (t * kInvSqrt2) * poly_estrin(E, z);
+    fk = poly_estrin(G, z);
+    // sum_m c_m He_{2m+1}(t) / sigma^{2m+1}: He1 = t, He3 = t^3 - 3t, He5 = t^5 - 10t^3 + 15t
+    const double is2 = is * is;
+    const double he3 = t * (t2 - 3.0);
+    const double he5 = t * fma(t2, t2 - 10.0, 15.0);
+    const double res = is * fma(is2, fma(is2 * (1.0 / 30240.0), he5, (-1.0 / 720.0) * he3), (1.0 / 12.0) * t);
+    return fma(-res, fk, sig * kSqrtHalfPi * erf_y) + 0.5 * fk - base;
+}
+
 // The capped kind with sigma >= 360 (q[7] == 1: NTRU / q-ary bases' large-sigma
 // coordinates), streamlined for latency -- the Klein kernels' per-coordinate
 // dependency chain runs through it: the quantile guess from a fixed fp64 erfinv
@@ -783,33 +832,25 @@ __device__ __forceinline__ double sample_z_capped(double mu, double u, const QHe
     const double sig = h.v[0], is = h.v[1];
     const double c = rint(mu);
     const double m = mu - c;
-    double S = q[kSzS + kSzDeg], base = q[kSzB + kSzDeg];
+    double cS[kSzDeg + 1], cB[kSzDeg + 1];
 #pragma unroll
-    for (int k = kSzDeg - 1; k >= 0; --k) {
-        S = fma(S, m, q[kSzS + k]);
-        base = fma(base, m, q[kSzB + k]);
+    for (int k = 0; k <= kSzDeg; ++k) {
+        cS[k] = q[kSzS + k];
+        cB[k] = q[kSzB + k];
     }
+    const double S = poly_estrin(cS, m), base = poly_estrin(cB, m);
     const double target = u * S;
     // continuous quantile x = m + sigma sqrt(2) erfinv(v): erfinv(v) = v R(v^2)
+    constexpr double RI[13] = {0.8862269447150851, 0.23200895985592382, 0.1278390124627034,
+                               0.07920907048159789, 0.16780265291085433, -0.8188084361376584,
+                               4.787814391235978, -17.187235185827564, 42.14891487326897,
+                               -68.64189227692192, 71.76515059941498, -43.593212219926436,
+                               11.853485934431038};
     const double v = fmin(fmax((target + base) * h.v[4], -0.8485), 0.8485);
-    const double w = v * v;
-    double r = 11.853485934431038;
-    r = fma(r, w, -43.593212219926436);
-    r = fma(r, w, 71.76515059941498);
-    r = fma(r, w, -68.64189227692192);
-    r = fma(r, w, 42.14891487326897);
-    r = fma(r, w, -17.187235185827564);
-    r = fma(r, w, 4.787814391235978);
-    r = fma(r, w, -0.8188084361376584);
-    r = fma(r, w, 0.16780265291085433);
-    r = fma(r, w, 0.07920907048159789);
-    r = fma(r, w, 0.1278390124627034);
-    r = fma(r, w, 0.23200895985592382);
-    r = fma(r, w, 0.8862269447150851);
-    const double xg = fma(h.v[5] * v, r, m);
+    const double xg = fma(h.v[5] * v, poly_estrin(RI, v * v), m);
     double kd = fmin(fmax(ceil(xg - 0.5), -500.0), 500.0);
     double fk;
-    double Ck = em_C_rel<3>(kd, m, sig, is, PolyErf{}, base, fk);
+    double Ck = capped_C(kd, m, sig, is, base, fk);
     if (__builtin_amdgcn_ballot_w64(!(Ck > target) || (kd > -500.0 && Ck - fk > target)) != 0) {
 #pragma nounroll
         for (int it = 0; it < 64 && Ck <= target && kd < 500.0; ++it) {  // move up

@@ -1204,36 +1204,42 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     if constexpr (OZ) pnz |= vo.nz != 0;
                 }
             };
-            near16(p_hi < 16 ? p_hi : 16, p_hi);
-            const int rows_l = p_hi - 16 < 16 ? p_hi - 16 : 16;
-            if (rows_l > 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                d4_t c[4];
+            // one copy of the 16-step near field for both sub-panels (a second inlined
+            // copy doubles the hot loop's code beyond the instruction cache)
+#pragma nounroll
+            for (int half = 0; half < 2; ++half) {
+                const int top = p_hi - 16 * half;
+                const int rows16 = top < 16 ? top : 16;
+                if (rows16 <= 0) break;
+                if (half == 1) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    d4_t c[4];
 #pragma unroll
-                for (int g = 0; g < 4; ++g) c[g] = (d4_t){0.0, 0.0, 0.0, 0.0};
-                const double* __restrict__ rx = a.rx + (size_t)pk * 256 + lane;
-                const ZT* __restrict__ zu = Z + p0 + (size_t)(p_hi - 16) * ldz + (size_t)kq * ldz + 4 * nq;
+                    for (int g = 0; g < 4; ++g) c[g] = (d4_t){0.0, 0.0, 0.0, 0.0};
+                    const double* __restrict__ rx = a.rx + (size_t)pk * 256 + lane;
+                    const ZT* __restrict__ zu = Z + p0 + (size_t)(p_hi - 16) * ldz + (size_t)kq * ldz + 4 * nq;
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) {
-                    const double av = rx[64 * kk];
-                    ZQuad<ZT> q;
-                    q.load(zu + (size_t)(4 * kk) * ldz);
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const double av = rx[64 * kk];
+                        ZQuad<ZT> q;
+                        q.load(zu + (size_t)(4 * kk) * ldz);
+#pragma unroll
+                        for (int g = 0; g < 4; ++g)
+                            c[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, q.get(g), c[g], 0, 0, 0);
+                    }
 #pragma unroll
                     for (int g = 0; g < 4; ++g)
-                        c[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, q.get(g), c[g], 0, 0, 0);
+#pragma unroll
+                        for (int reg = 0; reg < 4; ++reg) F[(kq + 4 * reg) * LDF + 4 * nq + g] += c[g][reg];
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[r] = F[r * LDF + lane];
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
                 }
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-#pragma unroll
-                    for (int reg = 0; reg < 4; ++reg) F[(kq + 4 * reg) * LDF + 4 * nq + g] += c[g][reg];
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[r] = F[r * LDF + lane];
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                near16(rows_l, p_hi - 16);
+                near16(rows16, top);
             }
             if constexpr (OZ) {  // visible to the block at the next panel's staging barrier
                 if (__builtin_amdgcn_ballot_w64(pnz) != 0 && lane == 0) atomicOr(&nzm[pk >> 5], 1u << (pk & 31));
