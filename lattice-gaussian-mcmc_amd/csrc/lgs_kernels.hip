@@ -152,35 +152,30 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         const int kind = __builtin_amdgcn_readfirstlane((int)qh.v[2]);
         const int q7 = __builtin_amdgcn_readfirstlane(qh.v[7] == 0.0 ? 0 : (qh.v[7] == 1.0 ? 1 : 2));
         if (CERT && kind == kSzSmall && q7 == 0) {
-            const double lo = floor(mu - qh.v[6]), hi = ceil(mu + qh.v[6]), is = qh.v[1];
-            if (hi - lo <= 3.0) {
-                double emax = -INFINITY, e2 = -INFINITY, kmax = lo;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const double t = ((lo + (double)k) - mu) * is;
-                    const double e = lo + (double)k <= hi ? -0.5 * (t * t) : -INFINITY;
-                    const bool top = e > emax;
-                    e2 = top ? emax : fmax(e2, e);
-                    kmax = top ? lo + (double)k : kmax;
-                    emax = top ? e : emax;
-                }
-                const double gap = emax - e2;
-                fast = gap > 745.2 && !(a.linear_probs && emax < -745.2) &&
-                       gap - 745.2 > 1.01 * dmu * (hi - lo) * (is * is) + 1e-12 * gap;
-                zi = kmax;
-                ln = emax;
-            }
+            // the heaviest window point is rint(mu) (d1 = |mu - rint(mu)| < 1/2 unless a
+            // tie, which fails the test); every other point lies >= 1 - d1 from mu, so
+            // its log-weight is below the top one by >= is^2 (1 - 2 d1) / 2 -- a lower
+            // bound of the gap the general path computes from the window's exponents
+            const double is = qh.v[1], is2 = is * is;
+            const double c = rint(mu), d1 = fabs(mu - c), t = d1 * is;
+            const double emax = -0.5 * (t * t);
+            const double gap = 0.5 * is2 * (1.0 - 2.0 * d1);
+            const double hl = ceil(mu + qh.v[6]) - floor(mu - qh.v[6]);
+            fast = gap > 745.2 && !(a.linear_probs && emax < -745.2) &&
+                   gap - 745.2 > 1.01 * dmu * hl * is2 + 1e-12 * gap;
+            zi = c;
+            ln = emax;
         }
         if (!fast) {
             const double u = rs.u((uint32_t)(a.d - 1 - i));
+            SzPair r;
 #ifndef LGS_NO_CAPPED_POLY
             if (kind == kSzCapped && q7 == 1)  // sigma >= 360: the streamlined capped leaf
-                zi = sz_finish<CERT>(sample_z_capped_leaf<CERT>(mu, u, rec, WL, dmu), mu, u, rec, a.precision,
-                                     a.linear_probs != 0, WL, etab, ln, dmu, amb);
+                r = sample_z_capped_leaf<CERT>(mu, u, rec, WL, dmu);
             else
 #endif
-                zi = sample_z_coord_t<CERT>(mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, ln, dmu,
-                                            amb);
+                r = sample_z_coord_leaf<CERT>(mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, dmu);
+            zi = sz_finish<CERT>(r, mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, ln, dmu, amb);
         }
         if (WL) lw += ln;
     }
