@@ -169,6 +169,18 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         if (!fast) {
             const double u = rs.u((uint32_t)(a.d - 1 - i));
             SzPair r;
+#ifdef LGS_DIAG_NO_GENERIC  // diagnostic builds only: cost of the generic call sites (NOT bit-exact)
+            if (kind == kSzCapped && q7 == 1) {
+                r = sample_z_capped_leaf<CERT>(mu, u, rec, WL, dmu);
+                amb = CERT && (__builtin_isnan(r.z) || __builtin_isnan(r.ln));
+                zi = __builtin_isnan(r.z) ? rint(mu) : r.z;
+                ln = amb ? 0.0 : r.ln;
+            } else {
+                zi = rint(mu);
+            }
+            if (false)
+#endif
+            {
 #ifndef LGS_NO_CAPPED_POLY
             if (kind == kSzCapped && q7 == 1)  // sigma >= 360: the streamlined capped leaf
                 r = sample_z_capped_leaf<CERT>(mu, u, rec, WL, dmu);
@@ -176,6 +188,7 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
 #endif
                 r = sample_z_coord_leaf<CERT>(mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, dmu);
             zi = sz_finish<CERT>(r, mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, ln, dmu, amb);
+            }
         }
         if (WL) lw += ln;
     }
