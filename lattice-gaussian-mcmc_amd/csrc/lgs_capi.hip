@@ -534,10 +534,11 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     // M = max_{j>i} |R_ij|, L1 = sum_{j>i} |R_ij|, u = 2^-53:
     //  * both sums of R_ij z_j against the exact one: the reference's sequential sum
     //    gamma_d, the blocked FMA / MFMA sums gamma_{d+40}  -> (2d+80) 1.1 u M Z1;
-    //  * int8-digit far field: R rounded to 2^(E-56) (u M / 2 per unit of z), and the
-    //    recombination of the 8 digit classes, 7 roundings of at most
-    //    sum_j (|R_ij| + 2^E/256)(|z_j| + 512) with 2^E <= 8 M  -> 2 u M Z1 in Cb,
-    //    7.1 u (512 L1 + 16 M d) in Ca;
+    //  * int8-digit far field: R rounded to 2^(E-8D) with D = kOzDigits, at most
+    //    2^(E-8D-1) <= 2^(2-8D) M = 2^(55-8D) u M per unit of z (u M / 2 at D = 7,
+    //    128 u M at D = 6), and the recombination of the D + 1 digit classes, D <= 7
+    //    roundings of at most sum_j (|R_ij| + 2^E/256)(|z_j| + 512) with 2^E <= 8 M
+    //    -> (2 + 2^(55-8D)) u M Z1 in Cb, 7.1 u (512 L1 + 16 M d) in Ca;
     //  * subtraction, reciprocal / division: 5 u |mu| (the kernels' 6e-16 |mu|).
     std::vector<double> cert(2 * dd, 0.0);
     {
@@ -551,7 +552,7 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
             }
             const double ir = 1.0 / std::fabs(R[i * dd + i]);
             const double ca = 1.01 * 7.1 * u * (512.0 * L1 + 16.0 * M * (double)d) * ir;
-            const double cb = 1.01 * (1.1 * g / (1.0 - g) + 2.0 * u) * M * ir;
+            const double cb = 1.01 * (1.1 * g / (1.0 - g) + (2.0 + std::ldexp(1.0, 55 - 8 * lgs::kOzDigits)) * u) * M * ir;
             cert[2 * i] = ca;
             cert[2 * i + 1] = cb;
             szc[i * lgs::kSzcStride + lgs::kSzCa] = ca;
@@ -615,8 +616,8 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
             }
     }
     // int8-digit far field (klein_mfma_kernel OZ): per 32-row panel, rows scaled by
-    // 2^E_i (|R_ij| 2^-E_i < 1/4 over the panel's far columns j >= p_hi) and split
-    // into 7 balanced base-256 digits (54 significant bits).
+    // 2^E_i (|R_ij| 2^-E_i < 1/4 over the panel's far columns j >= p_hi), rounded
+    // to 2^(E_i - 8 kOzDigits) and split into kOzDigits balanced base-256 digits.
     const int64_t npan32 = (d + 31) / 32;
     std::vector<double> rscale(dd, 1.0);
     std::vector<int64_t> rdoff(npan32 + 1, 0);
@@ -640,7 +641,7 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
                 rscale[row] = std::ldexp(1.0, E);
                 const int t = r >> 4, n = r & 15;
                 for (int64_t j = p_hi; j < d; ++j) {
-                    long long M = std::llrint(std::ldexp(R[(size_t)row * dd + j], 56 - E));
+                    long long M = std::llrint(std::ldexp(R[(size_t)row * dd + j], 8 * lgs::kOzDigits - E));
                     const int64_t kk = j - p_hi, ch = kk / 64, h = (kk % 64) / 16, e = kk % 16;
                     for (int a = lgs::kOzDigits; a >= 1; --a) {  // least significant digit first
                         const long long dg = ((M % 256) + 256 + 128) % 256 - 128;

@@ -711,17 +711,18 @@ struct ZQuad<int64_t> {
 // ---------------------------------------------------- int8-digit far field
 // F_i = sum_{j >= p_hi} R_ij x_j for the 32 rows of panel pk and the wave's 64
 // samples, exactly enough to stand in for fp64: rows scaled by 2^E_i and split
-// into 7 balanced base-256 digits r_a (|R 2^-E| < 1/4, 54 significant bits,
-// host: lgs_set_basis); coefficients x in [-32767, 32639] held in the int16
+// into kOzDigits = 6 balanced base-256 digits r_a (|R 2^-E| < 1/4, rounded to
+// 2^(E-48); host: lgs_set_basis, whose certificate bound covers the rounding); coefficients x in [-32767, 32639] held in the int16
 // history as y = x + 128, so x = 256 x1 + x0 with x1 = the high byte of y and
 // x0 = low byte ^ 0x80 (both signed): a digit plane is two byte permutes of the
 // raw int16 pairs, and x = 0 gives two zero planes.  Class c = a - b of r_a x_b
 // (weight 256^-c) is summed exactly in int32 on v_mfma_i32_16x16x64_i8
-// (|sum| <= 2 K 2^14 < 2^31 for d <= 32768); then F_i = 2^E_i sum_c 256^-c C_c.
+// (|sum| <= 2 K 2^14 < 2^31 for d <= 32768); then F_i = 2^E_i sum_c 256^-c C_c
+// (classes c = 0 .. kOzDigits).
 // Chunks whose two 32-row panels are zero in every sample of the block (bits of
 // nzm, set by the near field) contribute nothing and are skipped: no history
 // read, no slab, no MFMA.
-// Four passes (16 samples each) keep 2 row tiles x 8 classes = 64 accumulator
+// Four passes (16 samples each) keep 2 row tiles x 7 classes = 56 accumulator
 // VGPRs.  Row tile 1 (the upper sub-panel) goes to acc through the LDS tile;
 // tile 0 is parked in the per-wave scratch f0 and moved into the LDS tile once
 // the upper rows are loaded (the LDS tile is free during the upper sub-panel).
@@ -774,13 +775,14 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
     constexpr int NG = LGS_OZ_NG;
 #pragma unroll 1
     for (int gp = 0; gp < 4 / NG; ++gp) {
-        v4i32_t cc[NG][2][8];  // [group][row tile][class]
+        constexpr int NC = kOzDigits + 1;  // digit classes
+        v4i32_t cc[NG][2][NC];  // [group][row tile][class]
 #pragma unroll
         for (int q = 0; q < NG; ++q)
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int c = 0; c < 8; ++c) cc[q][t][c] = (v4i32_t){0, 0, 0, 0};
+                for (int c = 0; c < NC; ++c) cc[q][t][c] = (v4i32_t){0, 0, 0, 0};
         const int16_t* __restrict__ hb0 = a.h16 + (blk0 * a.h16_lanes + p0 + 16 * NG * gp + n) * 16;
         const int16_t* __restrict__ hb1 = hb0 + 16 * 16;  // group NG gp + 1: 16 lanes further
         v4i32_t pf[4];
@@ -855,9 +857,9 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
                 for (int reg = 0; reg < 4; ++reg) {
                     const int g = NG * gp + q;
                     const int row = 16 * t + 4 * h + reg;  // panel row = record index
-                    double sv = (double)cc[q][t][7][reg];
+                    double sv = (double)cc[q][t][NC - 1][reg];
 #pragma unroll
-                    for (int c = 6; c >= 0; --c) sv = fma(sv, 0.00390625, (double)cc[q][t][c][reg]);
+                    for (int c = NC - 2; c >= 0; --c) sv = fma(sv, 0.00390625, (double)cc[q][t][c][reg]);
                     const double fv = sv * rec[row * kRecStride + kRecScale];
                     if (t == 1) {
                         F[(4 * h + reg) * LDF + 16 * g + n] = fv;
