@@ -48,7 +48,10 @@ constexpr int kRecScale = kRecRs + 15;
 constexpr int kRecStride = kRecRs + 18;  // 46: 368 bytes, 16-byte multiple
 // int8-digit far field layout: per 32-row panel pk >= 1 (K = 32 pk far columns,
 // ceil(K/64) chunks of 64): [chunk][row tile t][digit a][lane][16 bytes]
-constexpr int kOzDigits = 6;  // R digits: 48 significant bits (the rounding adds 128 u M to Cb, lgs_set_basis)
+#ifndef LGS_OZ_DIGITS
+#define LGS_OZ_DIGITS 6
+#endif
+constexpr int kOzDigits = LGS_OZ_DIGITS;  // R digits: 48 significant bits (the rounding adds 128 u M to Cb, lgs_set_basis)
 constexpr int kOzMaxD = 32768;  // int32 class sums stay exact: 2 * K * 2^14 < 2^31
 constexpr int kSzRound = 0;    // sigma_i < 1e-10: round(mu), no draw
 constexpr int kSzSmall = 1;    // sigma_i < 4: <= 4-point exponent path / table walk

@@ -57,15 +57,26 @@ def bench_klein(name, reps):
     wall = (time.perf_counter() - t0) / reps
     k_ms, k_n = ctx.timing_get(_capi.KERNEL_KLEIN)
     b_ms, b_n = ctx.timing_get(_capi.KERNEL_BZ)
-    kern = k_ms / max(k_n, 1) * reps / max(reps, 1)
     per_call_k = k_ms / reps
+    # the reference-order kernel (LGS_EXACT_ORDER: sequential unfused mu, one
+    # coordinate at a time) on a smaller sample, beside the default certified one
+    ne = min(n, 65536 if d <= 1024 else 8192)
+    ze = torch.empty((d, ne), dtype=torch.int32, device="cuda")
+    ctx.klein(1, 0, ne, ze, None, None, f | _capi.LGS_EXACT_ORDER)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ctx.klein(1, ne, ne, ze, None, None, f | _capi.LGS_EXACT_ORDER)
+    torch.cuda.synchronize()
+    exact_s = time.perf_counter() - t0
     return {"bench": "klein", "config": name, "d": d, "samples_per_call": n,
             "samples_per_s": round(n / wall, 1), "ms_per_call": round(wall * 1e3, 3),
             "klein_kernel_ms_per_call": round(per_call_k, 3), "bz_ms_per_call": round(b_ms / reps, 3),
-            # d^2 flops per sample as if the back-substitution ran in fp64: a rate,
-            # not a hardware bound (the far field runs on int8 MFMA; bench.py's
-            # roofline reports executed work per unit from PMC counters)
-            "klein_fp64_equivalent_tflops": round(n * d * d / (per_call_k / 1e3) / 1e12, 2),
+            # algorithmic back-substitution multiply-adds (d(d-1)/2 per sample) per
+            # second: a rate, not a hardware bound (the far field runs on int8 MFMA
+            # and skips all-zero chunks; bench.py's roofline reports executed work
+            # per unit from PMC counters)
+            "klein_backsub_gmacs_per_s": round(n * d * (d - 1) / 2 / (per_call_k / 1e3) / 1e9, 1),
+            "exact_order_samples_per_s": round(ne / exact_s, 1), "exact_order_samples": ne,
             "basis_setup_s": round(setup, 2)}
 
 
