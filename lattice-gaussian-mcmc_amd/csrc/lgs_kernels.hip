@@ -1395,19 +1395,23 @@ __global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
 // gather folded into the pass that already reads every proposal (a separate
 // gather touches one proposal in T per cache line).  VEC: 8 (16-bit store) or 4
 // consecutive proposals per lane in one load (ldz and n multiples of that).
-template <typename ZT, typename OT, bool VEC>
+// RY coordinates per workgroup (vector path): the weights cnt and the chains'
+// final-state indices are loaded once for RY rows of the store instead of once
+// per row (they were 2-3x the coefficient bytes per row, from L2).
+template <typename ZT, typename OT, bool VEC, int RY = 1>
 __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict__ Z, int64_t ldz,
                                                             const int32_t* __restrict__ cnt, int64_t n,
                                                             int64_t T, const int64_t* __restrict__ fsel,
                                                             int d, int64_t chunk,
                                                             unsigned long long* mom,
                                                             OT* __restrict__ zs, int zs_cm, int64_t nc) {
-    const int i = blockIdx.y;
+    const int i0 = blockIdx.y * RY;
     const int64_t p0 = (int64_t)blockIdx.x * chunk;
     const int64_t p1 = p0 + chunk < n ? p0 + chunk : n;
-    const ZT* __restrict__ zr = Z + (size_t)i * ldz;
-    long long s1 = 0, s2 = 0;
-    auto put = [&](int64_t c, long long z) {
+    long long s1[RY], s2[RY];
+#pragma unroll
+    for (int r = 0; r < RY; ++r) s1[r] = s2[r] = 0;
+    auto put = [&](int i, int64_t c, long long z) {
         if (zs_cm)
             zs[(size_t)i * nc + c] = (OT)z;
         else
@@ -1420,7 +1424,10 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
         typedef int iv4_t __attribute__((ext_vector_type(4)));
         const double rT = 1.0 / (double)T;
         for (int64_t p = p0 + VW * (int64_t)threadIdx.x; p < p1; p += VW * 256) {
-            const zv_t zv = *(const zv_t*)(zr + p);
+            zv_t zv[RY];
+#pragma unroll
+            for (int r = 0; r < RY; ++r)
+                zv[r] = i0 + r < d ? *(const zv_t*)(Z + (size_t)(i0 + r) * ldz + p) : (zv_t){};
             int w[VW];
 #pragma unroll
             for (int g = 0; g < VW / 4; ++g) {
@@ -1429,17 +1436,19 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
                 for (int k = 0; k < 4; ++k) w[4 * g + k] = wv[k];
             }
 #pragma unroll
-            for (int k = 0; k < VW; ++k) {
-                if constexpr (sizeof(ZT) == 2) {  // z^2 < 2^30: one 32x32->64 multiply-add each
-                    const int z = zv[k];
-                    s1 += (long long)w[k] * z;
-                    s2 += (long long)w[k] * (z * z);
-                } else {
-                    const long long z = zv[k];
-                    s1 += w[k] * z;
-                    s2 += w[k] * z * z;
+            for (int r = 0; r < RY; ++r)
+#pragma unroll
+                for (int k = 0; k < VW; ++k) {
+                    if constexpr (sizeof(ZT) == 2) {  // z^2 < 2^30: one 32x32->64 multiply-add each
+                        const int z = zv[r][k];
+                        s1[r] += (long long)w[k] * z;
+                        s2[r] += (long long)w[k] * (z * z);
+                    } else {
+                        const long long z = zv[r][k];
+                        s1[r] += w[k] * z;
+                        s2[r] += w[k] * z * z;
+                    }
                 }
-            }
             if (fsel) {  // chains whose proposals touch [p, p + VW - 1] (one, two at a boundary)
                 // p / T through the fp64 reciprocal, corrected by one step (p < 2^32)
                 int64_t c = (int64_t)((double)p * rT);
@@ -1449,35 +1458,46 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
                     const int64_t k = fsel[c] - p;
 #pragma unroll
                     for (int e = 0; e < VW; ++e)
-                        if (k == e) put(c, (long long)zv[e]);
+                        if (k == e)
+#pragma unroll
+                            for (int r = 0; r < RY; ++r)
+                                if (i0 + r < d) put(i0 + r, c, (long long)zv[r][e]);
                 }
             }
         }
     } else {
+        const ZT* __restrict__ zr = Z + (size_t)i0 * ldz;
         for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
             const long long z = (long long)zr[p], w = cnt ? cnt[p] : 1;
-            s1 += w * z;
-            s2 += w * z * z;
+            s1[0] += w * z;
+            s2[0] += w * z * z;
             if (fsel) {
                 const int64_t c = (int64_t)((uint32_t)p / (uint32_t)T);  // n < 2^32 (checked by the caller)
-                if (fsel[c] == p) put(c, z);
+                if (fsel[c] == p) put(i0, c, z);
             }
         }
     }
-    __shared__ long long r1[256], r2[256];
-    r1[threadIdx.x] = s1;
-    r2[threadIdx.x] = s2;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) {
-            r1[threadIdx.x] += r1[threadIdx.x + o];
-            r2[threadIdx.x] += r2[threadIdx.x + o];
+    // wave sums by shuffles, then the 4 waves' partials through LDS
+    __shared__ long long r1[RY][4], r2[RY][4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < RY; ++r) {
+        long long a = s1[r], b = s2[r];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            a += __shfl_xor(a, o);
+            b += __shfl_xor(b, o);
         }
-        __syncthreads();
+        if (lane == 0) {
+            r1[r][wave] = a;
+            r2[r][wave] = b;
+        }
     }
-    if (threadIdx.x == 0) {
-        atomicAdd(mom + i, (unsigned long long)r1[0]);
-        atomicAdd(mom + d + i, (unsigned long long)r2[0]);
+    __syncthreads();
+    if ((int)threadIdx.x < RY && i0 + (int)threadIdx.x < d) {
+        const int r = threadIdx.x;
+        atomicAdd(mom + i0 + r, (unsigned long long)(r1[r][0] + r1[r][1] + r1[r][2] + r1[r][3]));
+        atomicAdd(mom + d + i0 + r, (unsigned long long)(r2[r][0] + r2[r][1] + r2[r][2] + r2[r][3]));
     }
 }
 
@@ -1998,13 +2018,15 @@ hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt,
                          int zs_cm, int64_t nc, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const int64_t chunk = 16384;  // multiple of 4
+    constexpr int RY = 4;  // rows per workgroup, vector path
     const dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
+    const dim3 gridv((unsigned)((n + chunk - 1) / chunk), (unsigned)((d + RY - 1) / RY));
     const int vw = zb == 2 ? 8 : 4;  // proposals per lane of the vector path
     const bool vec = ldz % vw == 0 && n % vw == 0 && ((uintptr_t)Z % (vw * (uintptr_t)zb)) == 0 &&
                      (!cnt || ((uintptr_t)cnt % 16) == 0);
     LGS_ZT(zb, ZT, LGS_ZT(ob, OT, {
         if (vec)
-            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, true>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc);
+            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, true, RY>), gridv, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc);
         else
             hipLaunchKernelGGL((moments_final_kernel<ZT, OT, false>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc);
     }));
