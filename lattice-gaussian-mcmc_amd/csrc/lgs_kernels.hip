@@ -799,7 +799,12 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
                 (void)h1;
             }
         };
+#ifdef LGS_OZ_PASS_BARRIER
         __syncthreads();  // previous pass done with both buffers
+#endif
+        // (no barrier needed here: the previous pass's chunk loop ended with one after
+        // its last slab reads, and pass 0 follows the panel's record-staging barrier,
+        // which also publishes nzm)
         int cur = next_live(0);
         int nxt = cur < nch ? next_live(cur + 1) : nch;
         if (cur < nch) {
