@@ -123,7 +123,7 @@ struct lgs_ctx {
     std::vector<BzCall> pending_i8;
     // scratch
     DevBuf Z, LW, V, sel, fsel, cnt, ccnt, flags, stage_a, stage_b, stage_c, stage_d, stage_e,
-        stage_f, stage_g, vs;
+        stage_f, stage_g, stage_h, stage_i, vs;
     int64_t max_props = 1 << 18;
     int zint = 2;  // internal coefficient store width (bytes): 16-bit, sticky 32-bit on overflow; LGS_ZINT=4 forces 32-bit
     // timing
@@ -897,6 +897,14 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
              int64_t n_steps, int32_t thin, void* z_state, double* logw_state, int32_t* state_init,
              int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
              uint32_t flags) {
+    return lgs_imhk_trace(c, seed, first_chain, nc, first_step, n_steps, thin, z_state, logw_state,
+                          state_init, accepts, z_samples, v_samples, moments, nullptr, nullptr, flags);
+}
+
+int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64_t first_step,
+                   int64_t n_steps, int32_t thin, void* z_state, double* logw_state, int32_t* state_init,
+                   int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
+                   double* logw_samples, uint8_t* accepted, uint32_t flags) {
     int rc = check_ctx(c);
     if (rc) return rc;
     if (nc < 0 || n_steps < 0 || thin < 1) return fail(LGS_ERR_INVALID, "bad nc/n_steps/thin");
@@ -957,6 +965,16 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         HIP_TRY(hipMemcpyAsync(lws, logw_state, nc * 8, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(init, state_init, nc * 4, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(acc, accepts, nc * 8, hipMemcpyHostToDevice, c->stream));
+    }
+    // per-step record: device buffers of the whole call (host pointers: copied back at the end)
+    double* lwk = logw_samples;
+    uint8_t* accs = accepted;
+    if (!dev && (logw_samples || accepted)) {
+        if ((rc = c->stage_h.reserve((size_t)std::max<int64_t>(nc * n_keep, 1) * 8)) ||
+            (rc = c->stage_i.reserve((size_t)std::max<int64_t>(nc * n_steps, 1))))
+            return rc;
+        lwk = logw_samples ? c->stage_h.as<double>() : nullptr;
+        accs = accepted ? (uint8_t*)c->stage_i.p : nullptr;
     }
     unsigned long long* mom = nullptr;
     if (moments) {
@@ -1051,6 +1069,10 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         aa.carry_col = carry ? npb : -1;
         aa.cnt = moments ? c->cnt.as<int32_t>() : nullptr;
         aa.cnt_carry = moments ? c->ccnt.as<int32_t>() : nullptr;
+        aa.lw_keep = lwk && kb > 0 ? lwk + first_keep : nullptr;
+        aa.lw_ld = n_keep;
+        aa.acc_step = accs ? accs + t0 : nullptr;
+        aa.acc_ld = n_steps;
         {
             Scope s(c, 2);
             HIP_TRY(lgs::launch::accept(aa, c->stream));
@@ -1101,6 +1123,10 @@ int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64
         HIP_TRY(hipMemcpyAsync(accepts, acc, nc * 8, hipMemcpyDeviceToHost, c->stream));
         if (moments)
             HIP_TRY(hipMemcpyAsync(moments, mom, (size_t)2 * d * 8, hipMemcpyDeviceToHost, c->stream));
+        if (logw_samples && n_keep > 0)
+            HIP_TRY(hipMemcpyAsync(logw_samples, lwk, (size_t)nc * n_keep * 8, hipMemcpyDeviceToHost, c->stream));
+        if (accepted && n_steps > 0)
+            HIP_TRY(hipMemcpyAsync(accepted, accs, (size_t)nc * n_steps, hipMemcpyDeviceToHost, c->stream));
     }
     return finish(c);
 }

@@ -128,6 +128,10 @@ struct AcceptArgs {
     int32_t* cnt;        // nullable, per proposal (zeroed by caller)
     int32_t* cnt_carry;  // nullable, per chain
     int64_t carry_col;   // >= 0: sel of a state carried in from before the block = carry_col + chain
+    double* lw_keep;     // nullable: log weight of kept state k of chain c at lw_keep[c * lw_ld + k]
+    int64_t lw_ld;
+    uint8_t* acc_step;   // nullable: 1 where step t of chain c accepted, at acc_step[c * acc_ld + t]
+    int64_t acc_ld;
 };
 
 // Per-series statistics (lgs_diag.hip series_stats_kernel).  Series s starts at

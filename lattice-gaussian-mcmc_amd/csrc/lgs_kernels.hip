@@ -1370,12 +1370,15 @@ __global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
             ratio = r < 1.0 ? r : 1.0;  // min(1.0, r); NaN -> 1.0 like Python's min
         }
         const double u = accept_uniform(a.seed, a.step0 + (uint32_t)t, chain);
-        if (u < ratio) {
+        const bool take = u < ratio;
+        if (take) {
             cur = p;
             lw_x = lw_y;
             ++acc;
         }
+        if (a.acc_step) a.acc_step[c * a.acc_ld + t] = take ? 1 : 0;
         if ((t + 1) % a.thin == 0) {
+            if (a.lw_keep) a.lw_keep[c * a.lw_ld + keep] = lw_x;
             if (a.sel) a.sel[c * a.n_keep + keep] = cur >= 0 ? cur : (a.carry_col >= 0 ? a.carry_col + c : -1);
             if (a.cnt) {
                 if (cur < 0)

@@ -42,7 +42,7 @@ LGS_COUNTER_FALLBACK = 1
 
 # every symbol include/lgs.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_destroy", "lgs_set_stream",
-           "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_lattice_points", "lgs_log_density", "lgs_sample_z", "lgs_timing_enable",
+           "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_imhk_trace", "lgs_lattice_points", "lgs_log_density", "lgs_sample_z", "lgs_timing_enable",
            "lgs_timing_get", "lgs_device_info", "lgs_series_stats", "lgs_gram",
            "lgs_jump_distance", "lgs_marginal_tvd", "lgs_set_decoder", "lgs_nearest_plane",
            "lgs_round_decode", "lgs_counter")
@@ -90,6 +90,9 @@ def load_library(path: str = LIB_PATH):
     L.lgs_imhk.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint64,
                            ctypes.c_int64, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                            ctypes.c_uint32]
+    L.lgs_imhk_trace.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint64,
+                                 ctypes.c_int64, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                 _vp, _vp, ctypes.c_uint32]
     L.lgs_lattice_points.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint32]
     L.lgs_log_density.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint32]
     L.lgs_sample_z.argtypes = [_vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int32, _vp, _vp,
@@ -237,16 +240,24 @@ class Context:
         raise AssertionError("unreachable")
 
     def imhk(self, seed, first_chain, n_chains, first_step, n_steps, thin, z_state, logw_state,
-             state_init, accepts, z_samples=None, v_samples=None, moments=None, flags=0):
+             state_init, accepts, z_samples=None, v_samples=None, moments=None, flags=0,
+             logw_samples=None, accepted=None):
+        """lgs_imhk; with logw_samples (n_chains x n_steps/thin float64) or accepted
+        (n_chains x n_steps uint8) lgs_imhk_trace, which also records each kept
+        state's log weight and each step's accept decision."""
         zt = "int64" if flags & LGS_Z64 else "int32"
         _check_bufs(flags, self.device, ((z_state, zt, "z_state"), (logw_state, "float64", "logw_state"),
                                          (state_init, "int32", "state_init"), (accepts, "int64", "accepts"),
                                          (z_samples, zt, "z_samples"), (v_samples, "float64", "v_samples"),
-                                         (moments, "int64", "moments")))
-        _check(_lib.lgs_imhk(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(first_chain),
-                             int(n_chains), int(first_step), int(n_steps), int(thin),
-                             _ptr(z_state), _ptr(logw_state), _ptr(state_init), _ptr(accepts),
-                             _ptr(z_samples), _ptr(v_samples), _ptr(moments), int(flags)))
+                                         (moments, "int64", "moments"), (logw_samples, "float64", "logw_samples"),
+                                         (accepted, "uint8", "accepted")))
+        args = (self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(first_chain), int(n_chains), int(first_step),
+                int(n_steps), int(thin), _ptr(z_state), _ptr(logw_state), _ptr(state_init), _ptr(accepts),
+                _ptr(z_samples), _ptr(v_samples), _ptr(moments))
+        if logw_samples is None and accepted is None:
+            _check(_lib.lgs_imhk(*args, int(flags)))
+        else:
+            _check(_lib.lgs_imhk_trace(*args, _ptr(logw_samples), _ptr(accepted), int(flags)))
 
     def lattice_points(self, z, v_out=None, flags=0):
         if isinstance(z, np.ndarray):

@@ -57,6 +57,8 @@ class IMHKSampler(DiscreteGaussianSampler):
         self._lw = np.zeros(1)
         self._init = np.zeros(1, dtype=np.int32)
         self._next_step = 1
+        self._sbuf = None  # look-ahead block served by step() (see _fill_steps)
+        self._step_block = 16
         logger.info(f"Initialized IMHK with burn-in={self.burn_in}")
 
     # ------------------------------------------------------------ set-up (imhk.py:68-100)
@@ -89,6 +91,7 @@ class IMHKSampler(DiscreteGaussianSampler):
         """Advance the chain n_steps; returns kept coefficient vectors (n_steps//thin, d)."""
         ctx = self.context
         n_keep = n_steps // thin
+        self._sbuf = None  # the chain moves past any look-ahead block
         for z64 in (False, True):
             zt = np.int64 if z64 else np.int32
             z_state = self._z.astype(zt)
@@ -119,10 +122,64 @@ class IMHKSampler(DiscreteGaussianSampler):
         out = None if zs is None else zs[0, :n_keep].astype(np.int64)
         return out, int(acc[0])
 
+    def _fill_steps(self, k: int):
+        """Draw the next k steps of the chain in one lgs_imhk_trace call: kept states,
+        their log weights, the per-step accept decisions and the lattice points.  The
+        chain's own state is not advanced here: step() moves it through the block one
+        step at a time, so the other methods continue from wherever step() left it
+        (every draw has a fixed Philox counter, so the block equals k single steps)."""
+        ctx = self.context
+        d = self.dimension
+        flags = self._flags()
+        for z64 in (False, True):
+            zt = np.int64 if z64 else np.int32
+            z_state = self._z.astype(zt)
+            lw = self._lw.copy()
+            init = self._init.copy()
+            acc = np.zeros(1, dtype=np.int64)
+            zs = np.zeros((1, k, d), dtype=zt)
+            lws = np.zeros((1, k))
+            accd = np.zeros((1, k), dtype=np.uint8)
+            try:
+                ctx.imhk(self.seed, self.chain_id, 1, self._next_step, k, 1, z_state, lw, init, acc,
+                         z_samples=zs, flags=flags | (_capi.LGS_Z64 if z64 else 0),
+                         logw_samples=lws, accepted=accd)
+            except _capi.LgsError as e:
+                if e.code == _capi.LGS_ERR_OVERFLOW and not z64:
+                    continue
+                raise
+            break
+        z = zs[0].astype(np.int64)
+        self._sbuf = {"z": z, "lw": lws[0].copy(), "acc": accd[0].astype(bool),
+                      "v": ctx.lattice_points(z), "first": self._next_step, "flags": flags, "pos": 0}
+
     def step(self) -> Tuple[np.ndarray, bool]:
-        """One MCMC step (imhk.py:141-177): (new_state, accepted)."""
-        _, a = self._run(1, 1, keep=False)
-        return self.current_state.copy(), bool(a)
+        """One MCMC step (imhk.py:141-177): (new_state, accepted).  Served from a
+        look-ahead block drawn in one launch (16 steps, doubling up to 1024 while the
+        caller keeps stepping), identical to launching every step on its own."""
+        b = self._sbuf
+        if (b is None or b["pos"] >= len(b["lw"]) or b["first"] + b["pos"] != self._next_step
+                or b["flags"] != self._flags()):
+            if b is not None and b["pos"] >= len(b["lw"]):
+                self._step_block = min(2 * self._step_block, 1024)
+            self._fill_steps(self._step_block)
+            b = self._sbuf
+        j = b["pos"]
+        b["pos"] = j + 1
+        first_init = not bool(self._init[0])
+        self._z = b["z"][j:j + 1].copy()
+        self._lw = b["lw"][j:j + 1].copy()
+        self._init = np.ones(1, dtype=np.int32)
+        self._next_step += 1
+        accepted = bool(b["acc"][j])
+        self.total_proposals += 1
+        self.accepted_proposals += int(accepted)
+        self.current_coeffs = self._z[0].astype(int)
+        self.current_state = b["v"][j].copy()
+        self.current_log_weight = float(self._lw[0])
+        if first_init:
+            logger.debug(f"Initialized chain at state with log weight {self.current_log_weight:.4f}")
+        return self.current_state.copy(), accepted
 
     def sample_single(self) -> np.ndarray:
         """imhk.py:179-194: burn-in on first use, then one step."""
