@@ -1472,6 +1472,68 @@ int lgs_marginal_tvd(lgs_ctx* c, int64_t d, const void* x1, int64_t n1, const vo
     return finish(c);
 }
 
+int lgs_column_range(lgs_ctx* c, int64_t d, const void* x, int64_t n, double* min_out, double* max_out,
+                     uint32_t flags) {
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    int xb = 8;
+    const int xt = xtype_of(flags, xb);
+    if (xt < 0 || d <= 0 || n <= 0) return fail(LGS_ERR_INVALID, "bad arguments");
+    if (!x || !min_out || !max_out) return fail(LGS_ERR_INVALID, "null buffer");
+    const bool dev = flags & LGS_DEVICE_PTRS;
+    if ((rc = reset_flags(c))) return rc;
+    const void* X = nullptr;
+    if ((rc = dev_in(c, dev, x, (size_t)n * d * xb, c->dg_x, X))) return rc;
+    if ((rc = c->dg_a.reserve((size_t)4 * d * 8))) return rc;
+    long long* mn = c->dg_a.as<long long>();
+    long long* mx = mn + d;
+    std::vector<long long> init(2 * d);
+    for (int64_t i = 0; i < d; ++i) {
+        init[i] = LLONG_MAX;
+        init[d + i] = LLONG_MIN;
+    }
+    HIP_TRY(hipMemcpyAsync(mn, init.data(), (size_t)2 * d * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(lgs::launch::hist_range(X, xt, n, (int)d, mn, mx, c->flags.as<unsigned int>(), c->stream));
+    double* lo = dev ? min_out : (double*)(mx + d);
+    double* hi = dev ? max_out : lo + d;
+    HIP_TRY(lgs::launch::hist_keys_to_f64(mn, mx, (int)d, lo, hi, c->stream));
+    if (!dev) {
+        HIP_TRY(hipMemcpyAsync(min_out, lo, (size_t)d * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(max_out, hi, (size_t)d * 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    rc = finish(c);
+    if (rc == LGS_ERR_NONFINITE)
+        return fail(LGS_ERR_NONFINITE, "column range: non-finite value (or |integer| > 2^53)");
+    return rc;
+}
+
+int lgs_histogram(lgs_ctx* c, int64_t d, const void* x, int64_t n, int64_t bins, const double* edges,
+                  const double* first_denom, int64_t* counts_out, uint32_t flags) {
+    int rc = check_ctx(c, false);
+    if (rc) return rc;
+    int xb = 8;
+    const int xt = xtype_of(flags, xb);
+    if (xt < 0 || d <= 0 || n < 0 || bins <= 0 || d * bins > (1LL << 31))
+        return fail(LGS_ERR_INVALID, "bad arguments");
+    if ((n > 0 && !x) || !edges || !first_denom || !counts_out) return fail(LGS_ERR_INVALID, "null buffer");
+    const bool dev = flags & LGS_DEVICE_PTRS;
+    if ((rc = reset_flags(c))) return rc;
+    const void *X = nullptr, *E = nullptr, *FD = nullptr;
+    if ((rc = dev_in(c, dev, x, (size_t)n * d * xb, c->dg_x, X)) ||
+        (rc = dev_in(c, dev, edges, (size_t)d * (bins + 1) * 8, c->dg_y, E)) ||
+        (rc = dev_in(c, dev, first_denom, (size_t)d * 2 * 8, c->dg_a, FD)))
+        return rc;
+    unsigned long long* cnt = (unsigned long long*)counts_out;
+    if (!dev) {
+        if ((rc = c->dg_b.reserve((size_t)d * bins * 8))) return rc;
+        cnt = c->dg_b.as<unsigned long long>();
+    }
+    HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)d * bins * 8, c->stream));
+    HIP_TRY(lgs::launch::hist_counts(X, xt, n, (int)d, bins, (const double*)E, (const double*)FD, cnt, c->stream));
+    if (!dev) HIP_TRY(hipMemcpyAsync(counts_out, cnt, (size_t)d * bins * 8, hipMemcpyDeviceToHost, c->stream));
+    return finish(c);
+}
+
 }  // extern "C"
 
 // ============================================================ decoding

@@ -507,6 +507,145 @@ __global__ __launch_bounds__(256) void tvd_sum_kernel(const unsigned int* __rest
     out[i] = 0.5 * acc;
 }
 
+// ------------------------------------------------------------ binned histogram
+// compute_tvd's histogram branch (convergence_diag.py:51-63): np.histogram with
+// `bins` equal-width bins over a shared range.  Pass 1 (hist_range_*) finds each
+// column's min / max in fp64 (integer data exact below 2^53) with 64-bit ordered
+// keys; the host then builds the edges exactly as numpy does (np.linspace).
+// Pass 2 bins every value with numpy's uniform-bin index arithmetic
+// (numpy/lib/_histograms_impl.py: f = ((x - first) / denom) * bins, truncated,
+// the last edge folded into the last bin, then the +-1 corrections against the
+// linspace edges), so the counts are numpy's counts.  Small d x bins: counts in
+// LDS per block (flattened element loop); otherwise one thread per column.
+__device__ __forceinline__ long long f64_key(double v) {  // order-preserving int64 key
+    const long long b = __double_as_longlong(v);
+    return b ^ ((b >> 63) & 0x7fffffffffffffffLL);
+}
+
+template <typename XT>
+__device__ __forceinline__ void range_one(XT v, long long& lo, long long& hi, bool& bad) {
+    const double x = (double)v;
+    if (!isfinite(x) || (sizeof(XT) == 8 && !std::is_same<XT, double>::value && fabs(x) > 9007199254740992.0)) {
+        bad = true;
+        return;
+    }
+    const long long k = f64_key(x);
+    lo = k < lo ? k : lo;
+    hi = k > hi ? k : hi;
+}
+
+template <typename XT>
+__global__ __launch_bounds__(256) void hist_range_cols_kernel(const XT* __restrict__ x, int64_t n, int d,
+                                                              int64_t rows_per_block, long long* mn,
+                                                              long long* mx, unsigned int* flags) {
+    const int i = blockIdx.y * 256 + threadIdx.x;
+    if (i >= d) return;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+    long long lo = 0x7fffffffffffffffLL, hi = -0x7fffffffffffffffLL - 1;
+    bool bad = false;
+    for (int64_t r = r0; r < r1; ++r) range_one<XT>(x[(size_t)r * d + i], lo, hi, bad);
+    if (r1 > r0) {
+        atomicMin(mn + i, lo);
+        atomicMax(mx + i, hi);
+    }
+    if (bad) atomicOr(flags, kFlagNonFinite);
+}
+
+// small d (<= kHistLdsCols): flattened grid-stride loop, per-block LDS keys
+constexpr int kHistLdsCols = 512;
+template <typename XT>
+__global__ __launch_bounds__(256) void hist_range_flat_kernel(const XT* __restrict__ x, int64_t total, int d,
+                                                              long long* mn, long long* mx,
+                                                              unsigned int* flags) {
+    __shared__ long long slo[kHistLdsCols], shi[kHistLdsCols];
+    for (int i = threadIdx.x; i < d; i += 256) {
+        slo[i] = 0x7fffffffffffffffLL;
+        shi[i] = -0x7fffffffffffffffLL - 1;
+    }
+    __syncthreads();
+    bool bad = false;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += stride) {
+        long long lo = 0x7fffffffffffffffLL, hi = -0x7fffffffffffffffLL - 1;
+        range_one<XT>(x[e], lo, hi, bad);
+        if (lo <= hi) {
+            const int i = (int)(e % d);
+            atomicMin(slo + i, lo);
+            atomicMax(shi + i, hi);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < d; i += 256) {
+        if (slo[i] <= shi[i]) {
+            atomicMin(mn + i, slo[i]);
+            atomicMax(mx + i, shi[i]);
+        }
+    }
+    if (bad) atomicOr(flags, kFlagNonFinite);
+}
+
+__global__ void hist_keys_to_f64_kernel(const long long* __restrict__ mn, const long long* __restrict__ mx,
+                                        int d, double* __restrict__ lo, double* __restrict__ hi) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= d) return;
+    auto un = [](long long k) { return __longlong_as_double(k ^ ((k >> 63) & 0x7fffffffffffffffLL)); };
+    lo[i] = un(mn[i]);
+    hi[i] = un(mx[i]);
+}
+
+// bin of one value (numpy's uniform-bin path; x already known to be in range)
+__device__ __forceinline__ int64_t hist_bin(double x, const double* __restrict__ e, double first,
+                                            double denom, int64_t nb) {
+    const double f = ((x - first) / denom) * (double)nb;
+    int64_t k = (int64_t)f;
+    if (k == nb) k -= 1;
+    if (x < e[k]) k -= 1;
+    if (x >= e[k + 1] && k != nb - 1) k += 1;
+    return k;
+}
+
+template <typename XT>
+__global__ __launch_bounds__(256) void hist_cols_kernel(const XT* __restrict__ x, int64_t n, int d,
+                                                        int64_t rows_per_block, int64_t nb,
+                                                        const double* __restrict__ edges,
+                                                        const double* __restrict__ fd,
+                                                        unsigned long long* __restrict__ cnt) {
+    const int i = blockIdx.y * 256 + threadIdx.x;
+    if (i >= d) return;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+    const double* e = edges + (size_t)i * (nb + 1);
+    const double first = fd[2 * i], denom = fd[2 * i + 1];
+    const double lo = e[0], hi = e[nb];
+    for (int64_t r = r0; r < r1; ++r) {
+        const double v = (double)x[(size_t)r * d + i];
+        if (v >= lo && v <= hi) atomicAdd(cnt + (size_t)i * nb + hist_bin(v, e, first, denom, nb), 1ull);
+    }
+}
+
+constexpr int kHistLdsBins = 8192;
+template <typename XT>
+__global__ __launch_bounds__(256) void hist_flat_kernel(const XT* __restrict__ x, int64_t total, int d,
+                                                        int64_t nb, const double* __restrict__ edges,
+                                                        const double* __restrict__ fd,
+                                                        unsigned long long* __restrict__ cnt) {
+    __shared__ unsigned int sc[kHistLdsBins];
+    const int nbins = d * (int)nb;
+    for (int k = threadIdx.x; k < nbins; k += 256) sc[k] = 0u;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t e0 = (int64_t)blockIdx.x * 256 + threadIdx.x; e0 < total; e0 += stride) {
+        const int i = (int)(e0 % d);
+        const double* e = edges + (size_t)i * (nb + 1);
+        const double v = (double)x[e0];
+        if (v >= e[0] && v <= e[nb]) atomicAdd(sc + i * nb + hist_bin(v, e, fd[2 * i], fd[2 * i + 1], nb), 1u);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nbins; k += 256)
+        if (sc[k]) atomicAdd(cnt + k, (unsigned long long)sc[k]);
+}
+
 // ============================================================ launchers
 namespace launch {
 
@@ -626,6 +765,45 @@ hipError_t tvd_sum(const unsigned int* c1, const unsigned int* c2, const long lo
                    int64_t n1, int64_t n2, double* out, hipStream_t st) {
     hipLaunchKernelGGL(tvd_sum_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, st, c1, c2, off, d,
                        (double)n1, (double)n2, out);
+    return hipGetLastError();
+}
+
+static unsigned flat_blocks(int64_t total) {
+    const int64_t b = (total + 4095) / 4096;  // ~16 elements per thread
+    return (unsigned)(b < 1 ? 1 : b > 2048 ? 2048 : b);
+}
+
+hipError_t hist_range(const void* x, int xtype, int64_t n, int d, long long* mn, long long* mx,
+                      unsigned int* flags, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if (d <= kHistLdsCols) {
+        const int64_t total = n * d;
+        LGS_XT(xtype, XT, hipLaunchKernelGGL(hist_range_flat_kernel<XT>, dim3(flat_blocks(total)), dim3(256), 0, st, (const XT*)x, total, d, mn, mx, flags));
+    } else {
+        const int64_t rpb = tvd_rows(n);
+        const dim3 grid((unsigned)((n + rpb - 1) / rpb), (unsigned)((d + 255) / 256));
+        LGS_XT(xtype, XT, hipLaunchKernelGGL(hist_range_cols_kernel<XT>, grid, dim3(256), 0, st, (const XT*)x, n, d, rpb, mn, mx, flags));
+    }
+    return hipGetLastError();
+}
+
+hipError_t hist_keys_to_f64(const long long* mn, const long long* mx, int d, double* lo, double* hi,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(hist_keys_to_f64_kernel, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, st, mn, mx, d, lo, hi);
+    return hipGetLastError();
+}
+
+hipError_t hist_counts(const void* x, int xtype, int64_t n, int d, int64_t nb, const double* edges,
+                       const double* fd, unsigned long long* cnt, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if ((int64_t)d * nb <= kHistLdsBins) {
+        const int64_t total = n * d;
+        LGS_XT(xtype, XT, hipLaunchKernelGGL(hist_flat_kernel<XT>, dim3(flat_blocks(total)), dim3(256), 0, st, (const XT*)x, total, d, nb, edges, fd, cnt));
+    } else {
+        const int64_t rpb = tvd_rows(n);
+        const dim3 grid((unsigned)((n + rpb - 1) / rpb), (unsigned)((d + 255) / 256));
+        LGS_XT(xtype, XT, hipLaunchKernelGGL(hist_cols_kernel<XT>, grid, dim3(256), 0, st, (const XT*)x, n, d, rpb, nb, edges, fd, cnt));
+    }
     return hipGetLastError();
 }
 

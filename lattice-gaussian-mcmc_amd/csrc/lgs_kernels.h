@@ -177,6 +177,15 @@ hipError_t tvd_hist(const void* x, int xtype, int64_t n, int d, const long long*
                     const long long* off, unsigned int* cnt, hipStream_t st);
 hipError_t tvd_sum(const unsigned int* c1, const unsigned int* c2, const long long* off, int d,
                    int64_t n1, int64_t n2, double* out, hipStream_t st);
+// binned histogram (compute_tvd's bins branch): per-column fp64 range as ordered
+// int64 keys (mn / mx must start at +/- the extreme key), converted by
+// hist_keys_to_f64; counts of numpy's equal-width bins ADDED to cnt (d x nb)
+hipError_t hist_range(const void* x, int xtype, int64_t n, int d, long long* mn, long long* mx,
+                      unsigned int* flags, hipStream_t st);
+hipError_t hist_keys_to_f64(const long long* mn, const long long* mx, int d, double* lo, double* hi,
+                            hipStream_t st);
+hipError_t hist_counts(const void* x, int xtype, int64_t n, int d, int64_t nb, const double* edges,
+                       const double* fd, unsigned long long* cnt, hipStream_t st);
 
 // zb / ob / ib: coefficient element width in bytes (2, 4 or 8)
 hipError_t klein(const KleinArgs& a, const double* R, const double* RP, const double* RC,

@@ -44,7 +44,7 @@ LGS_COUNTER_FALLBACK = 1
 EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_destroy", "lgs_set_stream",
            "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_imhk_trace", "lgs_lattice_points", "lgs_log_density", "lgs_sample_z", "lgs_timing_enable",
            "lgs_timing_get", "lgs_device_info", "lgs_series_stats", "lgs_gram",
-           "lgs_jump_distance", "lgs_marginal_tvd", "lgs_set_decoder", "lgs_nearest_plane",
+           "lgs_jump_distance", "lgs_marginal_tvd", "lgs_column_range", "lgs_histogram", "lgs_set_decoder", "lgs_nearest_plane",
            "lgs_round_decode", "lgs_counter")
 
 
@@ -108,6 +108,8 @@ def load_library(path: str = LIB_PATH):
     L.lgs_gram.argtypes = [_vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp, ctypes.c_uint32]
     L.lgs_jump_distance.argtypes = [_vp, _i64, _i64, _vp, _i64, _vp, ctypes.c_uint32]
     L.lgs_marginal_tvd.argtypes = [_vp, _i64, _vp, _i64, _vp, _i64, _vp, ctypes.c_uint32]
+    L.lgs_column_range.argtypes = [_vp, _i64, _vp, _i64, _vp, _vp, ctypes.c_uint32]
+    L.lgs_histogram.argtypes = [_vp, _i64, _vp, _i64, _i64, _vp, _vp, _vp, ctypes.c_uint32]
     L.lgs_set_decoder.argtypes = [_vp, _vp, _vp]
     L.lgs_nearest_plane.argtypes = [_vp, _i64, _vp, _vp, _vp, ctypes.c_uint32]
     L.lgs_round_decode.argtypes = [_vp, _i64, _vp, _vp, _vp, ctypes.c_uint32]
@@ -151,7 +153,7 @@ def _check_bufs(flags, device, bufs):
     context's device) -- a mismatch would be silently misread by the library."""
     dev_flag = bool(flags & LGS_DEVICE_PTRS)
     for a, want, name in bufs:
-        if a is None:
+        if a is None or isinstance(a, int):  # raw addresses are opaque: the caller vouches for them
             continue
         got = _dtype_name(a)
         if got != want:
@@ -361,6 +363,25 @@ class Context:
         d = x1.shape[1]
         _check(_lib.lgs_marginal_tvd(self._h, int(d), _ptr(x1), int(x1.shape[0]), _ptr(x2),
                                      int(x2.shape[0]), _ptr(out), int(flags | x_flags(x1))))
+
+    def column_range(self, x, lo, hi, flags=0):
+        """Per-column min / max (fp64) of row-major (n, d) samples into lo / hi (d)."""
+        n, d = x.shape
+        _check(_lib.lgs_column_range(self._h, int(d), _ptr(x), int(n), _ptr(lo), _ptr(hi),
+                                     int(flags | x_flags(x))))
+
+    def histogram(self, x, edges, first_denom, counts, flags=0):
+        """np.histogram counts per column: x (n, d), edges (d, bins+1), first_denom
+        (d, 2), counts (d, bins) int64 -- all host or all device (LGS_DEVICE_PTRS)."""
+        n, d = x.shape
+        bins = edges.shape[1] - 1
+        if tuple(edges.shape) != (d, bins + 1) or tuple(first_denom.shape) != (d, 2) or \
+                tuple(counts.shape) != (d, bins):
+            raise ValueError("histogram: edges (d, bins+1), first_denom (d, 2), counts (d, bins)")
+        _check_bufs(flags, self.device, ((edges, "float64", "edges"), (first_denom, "float64", "first_denom"),
+                                         (counts, "int64", "counts")))
+        _check(_lib.lgs_histogram(self._h, int(d), _ptr(x), int(n), int(bins), _ptr(edges),
+                                  _ptr(first_denom), _ptr(counts), int(flags | x_flags(x))))
 
     # ---------------------------------------------------------------- timing / info
     def timing_enable(self, on=True):

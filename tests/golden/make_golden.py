@@ -18,10 +18,12 @@ Per draw the generator also records
   * ``margin`` -- |u - nearest CDF boundary|,
 so tests can tell a legitimate near-tie apart from a real mismatch.
 
-Usage:  python3 -B tests/golden/make_golden.py   (writes tests/golden/*.npz)
+Usage:  python3 -B tests/golden/make_golden.py [--out DIR] [--only NAME ...]
+        (writes DIR/*.npz, default tests/golden; --only klein_ntru128 etc.)
 """
 from __future__ import annotations
 
+import argparse
 import os
 import sys
 
@@ -80,6 +82,7 @@ class Cursor:
 
 
 CUR = None
+OUT = HERE
 
 
 def choice_shim(a, size=None, replace=True, p=None):
@@ -159,13 +162,19 @@ def klein_fixture(name, B, sigma, n, seed, center=None, first=0, store_basis=Tru
     if store_basis:
         out["B"] = lat.basis
         out["v"] = V
-    else:  # large case: tests rebuild B and R; keep a digest of the reference's R
+    else:  # large case: tests rebuild B; the reference's R is stored as its upper
+        # triangle (LAPACK builds differ by ulps between hosts) plus, per row, whether
+        # the sign fix (klein.py:69-73) left -0.0 below the diagonal, and its digest
         import hashlib
-        del out["R"], out["cprime"]
-        out["R_sha256"] = hashlib.sha256(np.ascontiguousarray(s.R).tobytes()).hexdigest()
+        Rr = np.ascontiguousarray(s.R)
+        d = Rr.shape[0]
+        out["R_sha256"] = hashlib.sha256(Rr.tobytes()).hexdigest()
+        out["R_upper"] = Rr[np.triu_indices(d)]
+        out["R_lower_negzero_rows"] = np.array([i > 0 and bool(np.signbit(Rr[i, 0])) for i in range(d)])
+        del out["R"]
     if extra:
         out.update(extra)
-    np.savez_compressed(os.path.join(HERE, f"klein_{name}.npz"), **out)
+    np.savez_compressed(os.path.join(OUT, f"klein_{name}.npz"), **out)
     print(f"klein_{name}: n={n} d={lat.dimension} draws={len(log)} "
           f"min_margin={log[:, 1].min() if len(log) else 0:.3g} cache_flags={flags.sum()}")
 
@@ -205,7 +214,7 @@ def imhk_fixture(name, B, sigma, n_chains, n_steps, seed, center=None):
             R, cp = ps.R, ps.center_transformed
     finally:
         np.random.choice, np.random.rand = _np_choice, _np_rand
-    np.savez_compressed(os.path.join(HERE, f"imhk_{name}.npz"), name=name, sigma=sigma,
+    np.savez_compressed(os.path.join(OUT, f"imhk_{name}.npz"), name=name, sigma=sigma,
                         seed=np.uint64(seed), B=lat.basis, R=R, cprime=cp,
                         center=np.zeros(lat.dimension) if center is None else np.asarray(center),
                         z=np.array(Zs, dtype=np.int64), accepted=np.array(acc, dtype=bool),
@@ -239,33 +248,50 @@ def samplez_fixture(seed=7):
             u, m, _ = CUR.log[-1]
             rows.append((mu, sig, u, int(z), m))
     a = np.array(rows)
-    np.savez_compressed(os.path.join(HERE, "samplez_table.npz"), mu=a[:, 0], sigma=a[:, 1],
+    np.savez_compressed(os.path.join(OUT, "samplez_table.npz"), mu=a[:, 0], sigma=a[:, 1],
                         u=a[:, 2], z=a[:, 3].astype(np.int64), margin=a[:, 4])
     print(f"samplez_table: {len(rows)} decisions, min margin {a[:, 4].min():.3g}")
 
 
-def main():
+def fixtures():
+    """name -> generator of every fixture this script writes (in its order)."""
     seed = 0x5EED_1234_ABCD
-    samplez_fixture()
-    klein_fixture("Z64", np.eye(64), 5.0, 1024, seed)
-    klein_fixture("I2", np.eye(2), 2.0, 512, seed)
-    klein_fixture("B2", np.array([[4.0, 1.0], [1.0, 3.0]]), 2.0, 512, seed)
-    klein_fixture("B2_center", np.array([[4.0, 1.0], [1.0, 3.0]]), 2.0, 256, seed,
-                  center=[0.3, -1.7])
     rng = np.random.default_rng(11)
     G = rng.standard_normal((16, 16)) * 3 + np.eye(16) * 4
-    klein_fixture("gauss16", G, 7.5, 256, seed, center=rng.standard_normal(16))
+    cG = rng.standard_normal(16)
     # edge: sigma_i < 1e-10 (rounding, no draw) and sigma_i > 1e10 (clamped to 1e6)
     E = np.diag([1e12, 1e-11, 1.0, 3.0, 0.5, 7.0]) + np.triu(np.arange(36).reshape(6, 6) % 5, 1)
-    klein_fixture("edge6", E, 5.0, 128, seed, center=[0.5, 0.25, -2.0, 1.5, 0.0, 3.3])
-    klein_fixture("qary128", lattices.qary_basis(64, 64, 3329, 1), 165.7, 256, seed)
-    klein_fixture("ntru32", lattices.ntru_basis(16, 12289, 1), 165.7, 128, seed)
-    klein_fixture("ntru128", lattices.ntru_basis(64, 12289, 1), 165.7, 128, seed)
-    klein_fixture("ntru1024", lattices.ntru_basis(512, 12289, 1), 165.7, 4, seed,
-                  first=1 << 33, store_basis=False,
-                  extra={"ntru_n": 512, "ntru_q": 12289, "ntru_seed": 1})
-    imhk_fixture("ntru32", lattices.ntru_basis(16, 12289, 1), 165.7, 4, 64, seed)
-    imhk_fixture("B2", np.array([[4.0, 1.0], [1.0, 3.0]]), 2.0, 2, 200, seed)
+    B2 = np.array([[4.0, 1.0], [1.0, 3.0]])
+    return {
+        "samplez_table": lambda: samplez_fixture(),
+        "klein_Z64": lambda: klein_fixture("Z64", np.eye(64), 5.0, 1024, seed),
+        "klein_I2": lambda: klein_fixture("I2", np.eye(2), 2.0, 512, seed),
+        "klein_B2": lambda: klein_fixture("B2", B2, 2.0, 512, seed),
+        "klein_B2_center": lambda: klein_fixture("B2_center", B2, 2.0, 256, seed, center=[0.3, -1.7]),
+        "klein_gauss16": lambda: klein_fixture("gauss16", G, 7.5, 256, seed, center=cG),
+        "klein_edge6": lambda: klein_fixture("edge6", E, 5.0, 128, seed, center=[0.5, 0.25, -2.0, 1.5, 0.0, 3.3]),
+        "klein_qary128": lambda: klein_fixture("qary128", lattices.qary_basis(64, 64, 3329, 1), 165.7, 256, seed),
+        "klein_ntru32": lambda: klein_fixture("ntru32", lattices.ntru_basis(16, 12289, 1), 165.7, 128, seed),
+        "klein_ntru128": lambda: klein_fixture("ntru128", lattices.ntru_basis(64, 12289, 1), 165.7, 128, seed),
+        "klein_ntru1024": lambda: klein_fixture("ntru1024", lattices.ntru_basis(512, 12289, 1), 165.7, 4, seed,
+                                                first=1 << 33, store_basis=False,
+                                                extra={"ntru_n": 512, "ntru_q": 12289, "ntru_seed": 1}),
+        "imhk_ntru32": lambda: imhk_fixture("ntru32", lattices.ntru_basis(16, 12289, 1), 165.7, 4, 64, seed),
+        "imhk_B2": lambda: imhk_fixture("B2", B2, 2.0, 2, 200, seed),
+    }
+
+
+def main(argv=None):
+    global OUT
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=HERE)
+    ap.add_argument("--only", nargs="*")
+    args = ap.parse_args(argv)
+    OUT = args.out
+    os.makedirs(OUT, exist_ok=True)
+    fx = fixtures()
+    for name in args.only or list(fx):
+        fx[name]()
 
 
 if __name__ == "__main__":

@@ -6,7 +6,8 @@ seeded here (AR(1) series with short and long memory, an integer IMHK trace
 from the build's C oracle, integer sample sets); only inputs and outputs are
 stored.
 
-Usage:  python3 -B tests/golden/make_golden_diag.py   (writes tests/golden/diag_*.npz)
+Usage:  python3 -B tests/golden/make_golden_diag.py          (writes tests/golden/diag_*.npz)
+        python3 -B tests/golden/make_golden_diag.py binned   (only diag_tvd_binned.npz)
 """
 from __future__ import annotations
 
@@ -103,8 +104,48 @@ def main():
                         tvd_marg=np.array([cd.compute_tvd(a[:, i], b[:, i]) for i in range(6)]),
                         tvd_1d=np.float64(cd.compute_tvd(a1, b1)),
                         mixing=np.int64(cd.mixing_time_estimate([0.9, 0.5, 0.3, 0.2, 0.1])))
+    binned()
     print("wrote diag fixtures to", HERE)
 
 
+def binned():
+    """compute_tvd's histogram branch (convergence_diag.py:51-63, 64-72): float,
+    integer-valued and int32 / int64 sample sets, a constant column (the +-0.5
+    range expansion), bins = 1 .. 64; the per-column np.histogram counts the
+    reference forms are stored beside its TVDs."""
+    rng = np.random.default_rng(20261017)
+    cases = {
+        "f2d": (rng.standard_normal((2500, 5)) * [1, 3, 0.01, 50, 2] + [0, 1, 0, -7, 1e3],
+                rng.standard_normal((1700, 5)) * [1.2, 3, 0.01, 45, 2] + [0.1, 1, 0, -7, 1e3 + 0.3]),
+        "intval": (np.round(rng.standard_normal((3000, 4)) * [2, 40, 165.7, 0.4]),
+                   np.round(rng.standard_normal((2000, 4)) * [2.2, 38, 170, 0.4])),
+        "i64": (np.round(rng.standard_normal(4001) * 700).astype(np.int64),
+                np.round(rng.standard_normal(3000) * 650 + 3).astype(np.int64)),
+        "i32": (np.round(rng.standard_normal((1024, 3)) * [5, 5000, 1]).astype(np.int32),
+                np.round(rng.standard_normal((999, 3)) * [5, 5100, 1]).astype(np.int32)),
+        "const": (np.full((300, 2), 7.0), np.full((200, 2), 7.0)),
+    }
+    out = {}
+    for name, (a, b) in cases.items():
+        out[f"{name}_a"] = a
+        out[f"{name}_b"] = b
+        for bins in (1, 7, 10, 64):
+            out[f"{name}_tvd_{bins}"] = np.float64(cd.compute_tvd(a, b, bins=bins))
+            a2 = a.reshape(len(a), -1)
+            b2 = b.reshape(len(b), -1)
+            c1, c2 = [], []
+            for i in range(a2.shape[1]):
+                lo = min(a2[:, i].min(), b2[:, i].min())
+                hi = max(a2[:, i].max(), b2[:, i].max())
+                c1.append(np.histogram(a2[:, i], bins=bins, range=(lo, hi))[0])
+                c2.append(np.histogram(b2[:, i], bins=bins, range=(lo, hi))[0])
+            out[f"{name}_counts_a_{bins}"] = np.array(c1, dtype=np.int64)
+            out[f"{name}_counts_b_{bins}"] = np.array(c2, dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, "diag_tvd_binned.npz"), **out)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["binned"]:
+        binned()
+    else:
+        main()

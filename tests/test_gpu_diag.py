@@ -82,6 +82,54 @@ def test_gelman_rubin_tvd_mixing(D):
         D.compute_tvd(t["a"] + 0.5, t["b"])                             # not integer-valued
 
 
+@pytest.mark.parametrize("name", ["f2d", "intval", "i64", "i32", "const"])
+def test_binned_tvd_matches_reference(D, name):
+    """compute_tvd(..., bins=k) (convergence_diag.py:51-63): the device's
+    np.histogram counts equal numpy's, the TVD the reference's (bit-identical)."""
+    import torch
+    from lgs_amd.diagnostics import _gpu
+    t = load_golden("diag_tvd_binned.npz")
+    a, b = t[f"{name}_a"], t[f"{name}_b"]
+    for bins in (1, 7, 10, 64):
+        assert D.compute_tvd(a, b, bins=bins) == t[f"{name}_tvd_{bins}"], bins
+        ad = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+        bd = torch.from_numpy(np.ascontiguousarray(b)).cuda()
+        assert D.compute_tvd(ad, bd, bins=bins) == t[f"{name}_tvd_{bins}"], bins
+        # the counts themselves, through the C-ABI
+        a2 = np.ascontiguousarray(a.reshape(len(a), -1))
+        ctx = _gpu.context()
+        d = a2.shape[1]
+        lo, hi = np.empty(d), np.empty(d)
+        ctx.column_range(a2, lo, hi)
+        np.testing.assert_array_equal(lo, a2.min(axis=0))
+        np.testing.assert_array_equal(hi, a2.max(axis=0))
+        b2 = b.reshape(len(b), -1)
+        edges = np.empty((d, bins + 1))
+        fd = np.empty((d, 2))
+        for i in range(d):
+            mn = min(a2[:, i].min(), b2[:, i].min())
+            mx = max(a2[:, i].max(), b2[:, i].max())
+            edges[i], fd[i] = D.convergence_diag._bin_setup(mn, mx, bins)
+        c = np.empty((d, bins), dtype=np.int64)
+        ctx.histogram(a2, edges, fd, c)
+        np.testing.assert_array_equal(c, t[f"{name}_counts_a_{bins}"])
+
+
+def test_binned_tvd_edges(D):
+    """Histogram branch edge cases: values on every bin edge (the +-1 index
+    corrections), a NaN (the reference's range check raises ValueError), empty input."""
+    x = np.linspace(-3.0, 5.0, 81)      # many values exactly on the edges of 8 / 16 / 80 bins
+    y = np.concatenate([x, x[::3]])
+    for bins in (8, 16, 80, 81, 3):
+        assert D.compute_tvd(x, y, bins=bins) == O.tvd_binned(x, y, bins)
+    big = np.array([2 ** 52, 2 ** 52 + 1, -(2 ** 52), 5], dtype=np.int64)
+    assert D.compute_tvd(big, big[::-1].copy(), bins=5) == O.tvd_binned(big, big[::-1], 5)
+    with pytest.raises(ValueError):
+        D.compute_tvd(np.array([1.0, np.nan]), np.array([1.0, 2.0]), bins=4)
+    with pytest.raises(ValueError):
+        D.compute_tvd(np.array([]), np.array([1.0]), bins=4)
+
+
 @pytest.mark.parametrize("n,d,lo,hi", [(1, 5, -3, 3), (63, 130, -32639, 32640), (1000, 128, -200, 200),
                                        (4099, 257, -3000, 3000), (777, 33, -40000, 40000)])
 def test_gram_exact(D, n, d, lo, hi):
