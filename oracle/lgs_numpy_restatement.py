@@ -41,6 +41,7 @@ class NumpyKlein:
         self.sigma = float(sigma)
         self.precision = int(precision)
         self.d = self.R.shape[0]
+        self.P = np.arange(self.d)
         self._cache = {}
 
     def _probabilities(self, mean, sigma):  # klein.py:101-139 (log space)
@@ -69,22 +70,21 @@ class NumpyKlein:
         cdf /= cdf[-1]
         return int(support[np.searchsorted(cdf, u, side="right")])
 
-    def sample_single(self, uniform):  # klein.py:181-220
-        d = self.d
-        x = np.zeros(d, dtype=int)
-        R = self.R
-        for i in range(d - 1, -1, -1):
+    def sample_single(self, uniform):  # klein.py:181-220, same statements and indexing
+        x = np.zeros(self.d, dtype=int)
+        for i in range(self.d - 1, -1, -1):
             conditional_sum = 0.0
-            Ri = R[i]
-            for j in range(i + 1, d):
-                conditional_sum += Ri[j] * x[j]
+            for j in range(i + 1, self.d):
+                conditional_sum += self.R[i, j] * x[j]
             mean = (self.cp[i] - conditional_sum) / self.R_diag[i]
             s = self.sigma / abs(self.R_diag[i])
             if s < 1e-10:
                 x[i] = int(np.round(mean))
             else:
-                x[i] = self._sample_1d(mean, min(s, 1e6) if s > 1e10 else s, uniform(d - 1 - i))
-        return self.B @ x
+                x[i] = self._sample_1d(mean, min(s, 1e6) if s > 1e10 else s, uniform(self.d - 1 - i))
+        x_permuted = np.zeros_like(x)  # klein.py:214-218 (P = identity)
+        x_permuted[self.P] = x
+        return self.B @ x_permuted
 
 
 def _worker(args):
@@ -107,8 +107,20 @@ def timed_run(R, cp, B, sigma, *, processes, samples_per_process, seed=1):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     jobs = [(R, cp, B, sigma, seed, c, samples_per_process) for c in range(processes)]
-    with ctx.Pool(processes) as pool:
-        out = pool.map(_worker, jobs)
+    # one core per worker: the spawned interpreters must not fan B @ x out over
+    # BLAS threads (OMP_NUM_THREADS = 16 on the GPU box would oversubscribe the cores)
+    keys = ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS", "MKL_NUM_THREADS")
+    saved = {k: os.environ.get(k) for k in keys}
+    os.environ.update({k: "1" for k in keys})
+    try:
+        with ctx.Pool(processes) as pool:
+            out = pool.map(_worker, jobs)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     total = sum(n for n, _ in out)
     wall = max(t for _, t in out)
     return total / wall, total, float(np.mean([t for _, t in out]))
