@@ -24,7 +24,8 @@ region.  The 8-GPU workload of BASELINE configs[3] is
 
 Also reported: the dominant kernel's roofline (the Klein sampler, HIP-event
 timed on its launch stream; executed-work and HBM counters from the committed
-rocprofv3 profile of this command, profiles/r02*_klein_counters.json), the
+rocprofv3 profile of this command, profiles/r0*_klein_counters.json, used only
+when its build_id is the loaded library's), the
 certificate's redo count, a parity check of the timed run's final chain states
 against the oracle, and the CPU baselines (the C oracle over the host cores and
 the NumPy restatement of the reference's loop, one process per core).
@@ -72,6 +73,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--numpy-samples", type=int, default=24, help="Klein samples per process, NumPy baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-dist", action="store_true", help="N = 1 without the one-rank RCCL group")
     ap.add_argument("--counters", default=os.environ.get("LGS_COUNTERS_JSON", ""),
                     help="klein_counters.json of a rocprofv3 profile of this command (default: newest in profiles/)")
     return ap.parse_args()
@@ -122,86 +124,33 @@ def b_alg(d):
     return 8 * d * (d + 1) // 2 + 4 * d
 
 
-def load_counters(path, config):
+def build_id(path):
+    """sha256 (first 16 hex digits) of the HIP library file this process loaded."""
+    import hashlib
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def load_counters(path, config, bid):
     """Per-launch Klein-kernel counters of a rocprofv3 profile of this bench command
-    (tools/gpu_roofline.sh -> profiles/<tag>_klein_counters.json)."""
+    (tools/gpu_roofline.sh -> profiles/<tag>_klein_counters.json), used only when
+    the profile was taken of the same library build (its build_id); returns
+    (counters or None, path or None, "current" | "stale" | None)."""
     if not path:
-        cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r02*_klein_counters.json")))
+        cands = sorted(glob.glob(os.path.join(REPO, "profiles", "r0*_klein_counters.json")))
         cands = [c for c in cands if json.load(open(c)).get("config") == config]
-        path = cands[-1] if cands else ""
+        same = [c for c in cands if json.load(open(c)).get("build_id") == bid]
+        path = (same or cands or [""])[-1]
     if not path or not os.path.exists(path):
-        return None, None
-    return json.load(open(path)), os.path.relpath(path, REPO)
-
-
-class LagSums:
-    """Lag-L autocovariance sums of per-chain scalar series, continued across bench
-    steps through a ring of each chain's last L values.  int64 sums
-    (exact, order-independent) for integer series, fp64 otherwise.  One update is a
-    handful of device kernels: the ring starts as zeros, so pairs reaching before
-    the first step contribute nothing and only the pair counts (host integers)
-    need the history length."""
-
-    def __init__(self, torch, n_chains, L, dtype, device):
-        self.t, self.L = torch, L
-        self.ring = torch.zeros((n_chains, L), dtype=dtype, device=device)
-        self.have = 0
-        self.S = torch.zeros(L + 1, dtype=dtype, device=device)   # sum_t x_t x_{t-k}
-        self.N = np.zeros(L + 1, dtype=np.int64)                  # pairs per lag
-        self.S1 = torch.zeros(1, dtype=dtype, device=device)
-        self.n = 0
-
-    def update(self, x):
-        torch, L, h = self.t, self.L, self.have
-        nc, T = x.shape
-        xs = torch.cat([self.ring, x], 1)                      # (nc, L + T)
-        win = xs.unfold(1, T, 1).flip(1)                       # win[:, k] = xs[:, L - k : L - k + T]
-        self.S += (win * x[:, None, :]).sum((0, 2))
-        k = np.arange(L + 1)
-        self.N += nc * np.maximum(T - np.maximum(k - h, 0), 0)
-        self.S1 += x.sum()
-        self.n += x.numel()
-        self.ring = xs[:, T:].clone() if T < L else x[:, T - L:].clone()
-        self.have = min(L, h + T)
-
-    def parts(self):
-        t = self.t
-        dev = self.S.device
-        return [self.S, t.from_numpy(self.N).to(dev), self.S1, t.tensor([self.n], dtype=t.int64, device=dev)]
-
-    @staticmethod
-    def acf(S, N, S1, n):
-        """ACF_k = (mean of lag-k products - mean^2) / (mean of squares - mean^2)."""
-        m = S1 / n
-        c = S / np.maximum(N, 1) - m * m
-        return (c / c[0]).tolist() if c[0] > 0 else None
-
-
-def pack_f64(torch, parts):
-    """One fp64 tensor for the single all-reduce: int64 parts split into exact
-    32-bit halves (each sum of halves over <= 2^20 ranks stays below 2^53)."""
-    out, layout = [], []
-    for p in parts:
-        if p.dtype == torch.int64:
-            out += [(p >> 32).double(), (p & 0xFFFFFFFF).double()]
-            layout.append(("i", p.numel()))
-        else:
-            out.append(p.double())
-            layout.append(("f", p.numel()))
-    return torch.cat(out), layout
-
-
-def unpack_f64(torch, flat, layout):
-    res, o = [], 0
-    for kind, n in layout:
-        if kind == "i":
-            hi, lo = flat[o:o + n], flat[o + n:o + 2 * n]
-            res.append((hi.round().long() << 32) + lo.round().long())
-            o += 2 * n
-        else:
-            res.append(flat[o:o + n])
-            o += n
-    return res
+        return None, None, None
+    cnt = json.load(open(path))
+    rel = os.path.relpath(path, REPO)
+    if bid is None or cnt.get("build_id") != bid:
+        return None, rel, "stale"
+    return cnt, rel, "current"
 
 
 def main():
@@ -212,19 +161,27 @@ def main():
     import torch
     import torch.distributed as dist
     from lgs_amd import _capi
+    from lgs_amd import distributed as D
     from lgs_amd.lattices import build_config
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("LGS_ONE_DEVICE") == "1":  # rehearsal: every rank on device 0 (gloo)
         local = 0
+    torch.cuda.set_device(local)
+    backend = os.environ.get("LGS_DIST_BACKEND", "nccl")  # nccl = RCCL on ROCm
+    collective = "none"
     if world > 1:
-        torch.cuda.set_device(local)
-        backend = os.environ.get("LGS_DIST_BACKEND", "nccl")  # nccl = RCCL on ROCm
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        D.init_process_group(backend, local, world)
+        collective = backend
+    elif not args.no_dist:
+        # N = 1 runs the same collective as N > 1: a one-rank RCCL group (set up
+        # outside the timed region); if the box cannot form it, say so and go on
+        try:
+            D.init_process_group(backend, local, 1)
+            collective = backend
+        except Exception as e:  # noqa: BLE001
+            collective = f"none ({type(e).__name__}: {str(e)[:120]})"
     dev = torch.device("cuda", local)
 
     lat, sigma = build_config(args.config)
@@ -243,62 +200,38 @@ def main():
     T = args.imhk_steps
     first_chain = rank * nc
     seed = 0x5EED_0001
-    flags = _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR
-    if args.exact_order:
-        flags |= _capi.LGS_EXACT_ORDER
-    z_state = torch.zeros((d, nc), dtype=torch.int32, device=dev)
-    lw = torch.zeros(nc, dtype=torch.float64, device=dev)
-    init = torch.zeros(nc, dtype=torch.int32, device=dev)
-    acc = torch.zeros(nc, dtype=torch.int64, device=dev)
-    mom = torch.zeros(2 * d, dtype=torch.int64, device=dev)
-    v_samples = None if args.no_v else torch.empty((nc, T, d), dtype=torch.float64, device=dev)
-    nacf = min(nc, ACF_CHAINS)
-    binv_t = torch.from_numpy(binv_k).to(dev)
-    lag_z0 = LagSums(torch, nacf, ACF_LAGS, torch.int64, dev)
-    lag_vv = LagSums(torch, nacf, ACF_LAGS, torch.float64, dev)
+    flags = _capi.LGS_EXACT_ORDER if args.exact_order else 0
+    # the timed path is lgs_amd.distributed's StreamingShard: one lgs_imhk call per
+    # bench step, lag sums on the device, one all-reduce (tests/test_distributed.py
+    # drives the same class with the oracle over gloo, world 2)
+    advance = D.gpu_advance(ctx, seed, first_chain, nc, d, dev, flags=flags, block_steps=T, want_v=not args.no_v)
+    shard = D.StreamingShard(advance, nc, d, binv_row=binv_k, device=dev, lag_chains=ACF_CHAINS, lags=ACF_LAGS)
+    z_state = advance.state["z"]
+    nacf = shard.lag_chains
     torch.cuda.synchronize()
 
-    step_counter = [1]
-
-    def one_step():
-        ctx.imhk(seed, first_chain, nc, step_counter[0], T, 1, z_state, lw, init, acc,
-                 v_samples=v_samples, moments=mom, flags=flags)
-        step_counter[0] += T
-        if v_samples is not None:
-            vs = v_samples[:nacf]
-            lag_z0.update(torch.round(vs @ binv_t).long())
-            lag_vv.update((vs * vs).sum(-1) * 1e-6)
-
-    def reduce_stats():
-        flat, layout = pack_f64(torch, [acc.sum().reshape(1), mom] + lag_z0.parts() + lag_vv.parts())
-        if world > 1:
-            dist.all_reduce(flat)  # the single collective (RCCL over xGMI)
-        return unpack_f64(torch, flat, layout)
-
     for _ in range(args.warmup):
-        one_step()
-    reduce_stats()  # warm torch's lazily loaded kernels and the communicator
-    acc.zero_()
-    mom.zero_()
-    lag_z0 = LagSums(torch, nacf, ACF_LAGS, torch.int64, dev)
-    lag_vv = LagSums(torch, nacf, ACF_LAGS, torch.float64, dev)
+        shard.step(T)
+    shard.reduce()  # warm torch's lazily loaded kernels and the communicator
+    shard.reset_stats()
     ctx.resolved(reset=True)
     ctx.timing_enable(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if D.collective_active():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        one_step()
-    stats = reduce_stats()
+        shard.step(T)
+    stats = shard.reduce()
     torch.cuda.synchronize()
-    if world > 1:
+    if D.collective_active():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    step_counter = [shard.next_step]
 
     proposals = args.steps * nc * T * world
     value = proposals / elapsed
@@ -307,13 +240,10 @@ def main():
     a_ms, a_n = ctx.timing_get(_capi.KERNEL_ACCEPT)
     m_ms, m_n = ctx.timing_get(_capi.KERNEL_MOMENTS)
     redos = ctx.resolved()
-    s_acc = int(stats[0].item())
+    s_acc = int(stats["accepts"][0].item())
     acceptance = s_acc / proposals
-    sz = [x.cpu().numpy() for x in stats[2:6]]
-    sv = [x.cpu().numpy() for x in stats[6:10]]
     acf = {"lags": ACF_LAGS, "chains": nacf * world,
-           "z_last": LagSums.acf(sz[0].astype(np.float64), sz[1], float(sz[2][0]), float(sz[3][0])),
-           "norm_v_sq": LagSums.acf(sv[0], sv[1], float(sv[2][0]), float(sv[3][0]))}
+           "z_last": D.StreamingShard.acf(stats["lag_z"]), "norm_v_sq": D.StreamingShard.acf(stats["lag_v"])}
 
     # ---- parity: the timed run's final chain states against the oracle.  In the
     # reference's IMHK mode every proposal is accepted (the weight is a constant up to
@@ -335,7 +265,7 @@ def main():
             parity = "skipped: acceptance < 1 (final state is not the last proposal)"
 
     if rank != 0:
-        if world > 1:
+        if D.collective_active():
             dist.destroy_process_group()
         return
 
@@ -347,10 +277,14 @@ def main():
     # command (per launch), so every fraction is of work actually issued.
     units = nc * T
     k_avg_s = (k_ms / max(k_n, 1)) / 1e3
-    cnt, cnt_path = load_counters(args.counters, args.config)
+    bid = build_id(_capi.LIB_PATH)
+    cnt, cnt_path, cnt_state = load_counters(args.counters, args.config, bid)
     roofline = {"bound": "mfma", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS, "achieved": None, "frac": None,
                 "traffic": None, "kernel": "klein_exact_kernel" if args.exact_order else "klein_mfma_kernel",
-                "kernel_ms_avg": round(k_avg_s * 1e3, 3), "units_per_launch": units}
+                "kernel_ms_avg": round(k_avg_s * 1e3, 3), "units_per_launch": units, "build_id": bid,
+                "counters": cnt_state if cnt_state != "current" else cnt_path}
+    if cnt_state == "stale":
+        roofline["counters_note"] = f"newest profile {cnt_path} is of another library build: not used"
     if cnt and cnt.get("units_per_launch") == units:
         f64 = cnt["fp64_flops"]
         roofline.update({
@@ -364,8 +298,7 @@ def main():
                     "traffic_over_compulsory": round(cnt["hbm_bytes"] / cnt["compulsory_bytes"], 2)},
             "int8_mfma": {"achieved_TOPS": round(cnt["i8_ops"] / k_avg_s / 1e12, 2),
                           "frac_of_5POPS": round(cnt["i8_ops"] / k_avg_s / 1e12 / I8_PEAK_TOPS, 4)},
-            "issue": cnt["issue"],
-            "counters": cnt_path})
+            "issue": cnt["issue"]})
     roofline["hbm_algorithmic_note"] = (
         f"SURVEY 8d B_alg = {b_alg(d)} B/sample counts R once per sample, but R is shared by every "
         f"chain (read once per 256-sample block from L2), so B_alg x rate is not an HBM quantity")
@@ -420,8 +353,9 @@ def main():
         "config": {"workload": f"{args.config}: {WORKLOADS[args.config]['text']}",
                    "chains_per_gpu": nc, "chains_total": nc * world, "imhk_steps_per_step": T, "thin": 1,
                    "lattice_points": not args.no_v, "kernel_order": "exact" if args.exact_order else "certified-blocked",
-                   "parallelism": f"chains sharded over {world} GPU(s); one RCCL all-reduce of every accumulator "
-                                  f"after the timed steps (inside the timed region)"},
+                   "parallelism": f"chains sharded over {world} GPU(s); one all-reduce of every accumulator "
+                                  f"after the timed steps (inside the timed region)",
+                   "collective": collective},
         "imhk_acceptance": round(acceptance, 6),
         "imhk_acceptance_cpu_reference": None if cpu is None else cpu["acceptance"],
         "parity_check": parity,
@@ -435,7 +369,7 @@ def main():
         "device": dinfo["name"],
     }
     print(json.dumps(out))
-    if world > 1:
+    if D.collective_active():
         dist.destroy_process_group()
 
 

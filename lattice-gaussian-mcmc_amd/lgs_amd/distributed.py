@@ -7,15 +7,29 @@ chains, each reseeded with ``seed + 1000 * chain_id``
 Here one process drives one GPU; global chain ids are split contiguously, and
 because every draw is addressed by (seed, global chain, step, slot) the union of
 the ranks' chains is bit-identical for any world size.  The only exchange is one
-all-reduce (RCCL over xGMI with the "nccl" backend, gloo on CPU) of the integer
-accumulators: accepted proposals and sum z / sum z^2 over kept states (plus,
-on request, the exact d x d second-moment matrix sum z z^T -- SURVEY §2.2 K4, about
-8 MB at d = 1024), and one all-gather of per-chain scalar statistics (mean and
-sum of squared deviations of a chosen coordinate over each chain's kept states)
-for the Gelman-Rubin statistic across every chain of the job.
+all-reduce (RCCL over xGMI with the "nccl" backend, gloo on CPU) of the
+accumulators, packed into one fp64 tensor (``allreduce_parts``; int64 sums split
+into exact 32-bit halves): accepted proposals and sum z / sum z^2 over kept
+states, plus on request the exact d x d second-moment matrix sum z z^T (SURVEY
+§2.2 K4, about 8 MB at d = 1024) or the lag-L autocovariance sums of scalar
+functionals of the kept states (``LagSums``); and one all-gather of
+per-chain scalar statistics (mean and sum of squared deviations of a chosen
+coordinate over each chain's kept states) for the Gelman-Rubin statistic.
+
+Two drivers share that reduction: ``imhk_sharded`` (one job, statistics back on
+the host) and ``StreamingShard`` (the benchmark's timed path: chains advanced
+block by block on the device, lag sums carried across blocks, one all-reduce at
+the end).  Both take the per-rank compute as a callable, so the CPU tests drive
+them with the oracle over gloo and the GPU path with the HIP C-ABI over RCCL.
+
+The collective is deliberately host-side ``torch.distributed`` rather than a
+C-ABI entry: the process group owns the RCCL communicator (one
+process per GPU), and the reduced data is a few KB once per job.
 """
 from __future__ import annotations
 
+import os
+import socket
 from dataclasses import dataclass
 from typing import Callable, Optional
 
@@ -27,6 +41,196 @@ def shard_range(n_total: int, rank: int, world: int):
     base, rem = divmod(int(n_total), int(world))
     first = rank * base + min(rank, rem)
     return first, base + (1 if rank < rem else 0)
+
+
+def collective_active() -> bool:
+    """A torch.distributed process group is initialised (any world size, 1 included:
+    the all-reduce then runs through the backend too)."""
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
+def init_process_group(backend: str, local_rank: int, world: int, rank: int = 0):
+    """Initialise torch.distributed for this rank: "nccl" (= RCCL on ROCm) binds the
+    communicator to cuda:local_rank; gloo on CPU.  Without a launcher's environment
+    (world 1) a local TCP store on 127.0.0.1 is used."""
+    import torch
+    import torch.distributed as dist
+    kw = {}
+    if "RANK" not in os.environ or "WORLD_SIZE" not in os.environ:
+        kw = dict(rank=rank, world_size=world)
+    if "MASTER_ADDR" not in os.environ:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        kw["init_method"] = f"tcp://127.0.0.1:{port}"
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), **kw)
+    else:
+        dist.init_process_group(backend, **kw)
+
+
+def pack_f64(torch, parts):
+    """One fp64 tensor for the single all-reduce: int64 parts split into exact
+    32-bit halves (each sum of halves over <= 2^20 ranks stays below 2^53)."""
+    out, layout = [], []
+    for p in parts:
+        if p.dtype == torch.int64:
+            out += [(p >> 32).double(), (p & 0xFFFFFFFF).double()]
+            layout.append(("i", p.numel(), tuple(p.shape)))
+        else:
+            out.append(p.double().reshape(-1))
+            layout.append(("f", p.numel(), tuple(p.shape)))
+    return torch.cat([o.reshape(-1) for o in out]), layout
+
+
+def unpack_f64(torch, flat, layout):
+    res, o = [], 0
+    for kind, n, shape in layout:
+        if kind == "i":
+            hi, lo = flat[o:o + n], flat[o + n:o + 2 * n]
+            res.append(((hi.round().long() << 32) + lo.round().long()).reshape(shape))
+            o += 2 * n
+        else:
+            res.append(flat[o:o + n].reshape(shape))
+            o += n
+    return res
+
+
+def allreduce_parts(parts, group=None):
+    """Sum a list of int64 / fp64 tensors (one device) over all ranks with ONE
+    all-reduce; int64 parts stay exact.  Without a process group: the local values."""
+    import torch
+    import torch.distributed as dist
+    flat, layout = pack_f64(torch, parts)
+    if collective_active():
+        dist.all_reduce(flat, group=group)  # the single collective (RCCL over xGMI / gloo)
+    return unpack_f64(torch, flat, layout)
+
+
+class LagSums:
+    """Lag-L autocovariance sums of per-chain scalar series, continued across
+    blocks through a ring of each chain's last L values.  int64 sums
+    (exact, order-independent) for integer series, fp64 otherwise.  One update is a
+    handful of device kernels: the ring starts as zeros, so pairs reaching before
+    the first step contribute nothing and only the pair counts (host integers)
+    need the history length."""
+
+    def __init__(self, torch, n_chains, L, dtype, device):
+        self.t, self.L = torch, L
+        self.ring = torch.zeros((n_chains, L), dtype=dtype, device=device)
+        self.have = 0
+        self.S = torch.zeros(L + 1, dtype=dtype, device=device)   # sum_t x_t x_{t-k}
+        self.N = np.zeros(L + 1, dtype=np.int64)                  # pairs per lag
+        self.S1 = torch.zeros(1, dtype=dtype, device=device)
+        self.n = 0
+
+    def update(self, x):
+        torch, L, h = self.t, self.L, self.have
+        nc, T = x.shape
+        xs = torch.cat([self.ring, x], 1)                      # (nc, L + T)
+        win = xs.unfold(1, T, 1).flip(1)                       # win[:, k] = xs[:, L - k : L - k + T]
+        self.S += (win * x[:, None, :]).sum((0, 2))
+        k = np.arange(L + 1)
+        self.N += nc * np.maximum(T - np.maximum(k - h, 0), 0)
+        self.S1 += x.sum()
+        self.n += x.numel()
+        self.ring = xs[:, T:].clone() if T < L else x[:, T - L:].clone()
+        self.have = min(L, h + T)
+
+    def parts(self):
+        t = self.t
+        dev = self.S.device
+        return [self.S, t.from_numpy(self.N).to(dev), self.S1, t.tensor([self.n], dtype=t.int64, device=dev)]
+
+    @staticmethod
+    def acf(S, N, S1, n):
+        """ACF_k = (mean of lag-k products - mean^2) / (mean of squares - mean^2)."""
+        m = S1 / n
+        c = S / np.maximum(N, 1) - m * m
+        return (c / c[0]).tolist() if c[0] > 0 else None
+
+
+class StreamingShard:
+    """One rank's shard of a streaming IMHK job -- the benchmark's timed path.
+
+    ``advance(first_step, n_steps, acc, mom)`` advances this rank's chains by
+    n_steps (adding accepted proposals per chain to ``acc`` and sum z / sum z^2 of
+    the kept states to ``mom``) and returns their kept lattice points v
+    (n_chains x n_steps x d, fp64 tensor) or None.  The shard carries the lag-L
+    autocovariance sums of two scalar functionals of the first ``lag_chains``
+    chains' kept states -- the coefficient z_k = round(<binv_row, v>) and
+    1e-6 ||v||^2 -- across blocks, and ``reduce`` combines everything over the
+    ranks with one all-reduce."""
+
+    def __init__(self, advance: Callable, n_chains: int, d: int, *, binv_row, device, lag_chains: int = 1024,
+                 lags: int = 16, first_step: int = 1):
+        import torch
+        self.t = torch
+        self.advance = advance
+        self.nc, self.d, self.dev = n_chains, d, device
+        self.lag_chains = min(n_chains, lag_chains)
+        self.lags = lags
+        self.binv = torch.as_tensor(np.asarray(binv_row, dtype=np.float64)).to(device)
+        self.next_step = first_step
+        self.reset_stats()
+
+    def reset_stats(self):
+        t = self.t
+        self.acc = t.zeros(self.nc, dtype=t.int64, device=self.dev)
+        self.mom = t.zeros(2 * self.d, dtype=t.int64, device=self.dev)
+        self.lag_z = LagSums(t, self.lag_chains, self.lags, t.int64, self.dev)
+        self.lag_v = LagSums(t, self.lag_chains, self.lags, t.float64, self.dev)
+        self.steps_done = 0
+
+    def step(self, n_steps: int):
+        v = self.advance(self.next_step, n_steps, self.acc, self.mom)
+        self.next_step += n_steps
+        self.steps_done += n_steps
+        if v is not None:
+            vs = v[:self.lag_chains]
+            self.lag_z.update(self.t.round(vs @ self.binv).long())
+            self.lag_v.update((vs * vs).sum(-1) * 1e-6)
+
+    def reduce(self, group=None) -> dict:
+        """One all-reduce of [accepts, moments, lag sums of both functionals]."""
+        parts = [self.acc.sum().reshape(1), self.mom] + self.lag_z.parts() + self.lag_v.parts()
+        r = allreduce_parts(parts, group=group)
+        return {"accepts": r[0], "moments": r[1], "lag_z": r[2:6], "lag_v": r[6:10]}
+
+    @staticmethod
+    def acf(parts):
+        S, N, S1, n = [x.cpu().numpy() for x in parts]
+        return LagSums.acf(S.astype(np.float64), N, float(S1[0]), float(n[0]))
+
+
+def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device, *, flags: int = 0,
+                block_steps: int = 0, want_v: bool = True):
+    """StreamingShard's advance over the HIP C-ABI: chain state resident on the
+    device (coordinate-major z), one lgs_imhk call per block; v of every kept state
+    into a preallocated (n_chains, block_steps, d) buffer.  The state tensors are
+    exposed as ``advance.state``."""
+    import torch
+    from . import _capi
+    st = {"z": torch.zeros((d, n_chains), dtype=torch.int32, device=device),
+          "lw": torch.zeros(n_chains, dtype=torch.float64, device=device),
+          "init": torch.zeros(n_chains, dtype=torch.int32, device=device),
+          "v": torch.empty((n_chains, block_steps, d), dtype=torch.float64, device=device)
+          if want_v and block_steps else None}
+    fl = flags | _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR
+
+    def advance(first_step, n_steps, acc, mom):
+        v = st["v"]
+        if want_v and (v is None or v.shape[1] != n_steps):
+            v = st["v"] = torch.empty((n_chains, n_steps, d), dtype=torch.float64, device=device)
+        ctx.imhk(seed, first_chain, n_chains, first_step, n_steps, 1, st["z"], st["lw"], st["init"], acc,
+                 v_samples=v if want_v else None, moments=mom, flags=fl)
+        return v if want_v else None
+
+    advance.state = st
+    return advance
 
 
 @dataclass
@@ -120,20 +324,15 @@ def imhk_sharded(compute: Callable, n_chains: int, n_steps: int, *, rank: int, w
 
     first, count = shard_range(n_chains, rank, world)
     r = compute(first_chain=first, n_chains=count, first_step=first_step, n_steps=n_steps)
-    parts = [[r.accepts, r.kept], r.moments.ravel()]
+    parts = [torch.tensor([r.accepts, r.kept], dtype=torch.int64),
+             torch.from_numpy(np.ascontiguousarray(r.moments, dtype=np.int64))]
     if r.gram is not None:
-        parts.append(r.gram.ravel())
-    stats = torch.from_numpy(np.concatenate(parts).astype(np.int64))
+        parts.append(torch.from_numpy(np.ascontiguousarray(r.gram, dtype=np.int64)))
     if device is not None:
-        stats = stats.to(device)
-    if world > 1:
-        dist.all_reduce(stats, group=group)  # the single reduction
-    s = stats.cpu().numpy()
-    d2 = r.moments.size
-    gram = None
-    if r.gram is not None:
-        d = d2 // 2
-        gram = s[2 + d2:].reshape(d, d)
+        parts = [p.to(device) for p in parts]
+    red = [p.cpu().numpy() for p in allreduce_parts(parts, group=group)]  # the single reduction
+    s = red[0]
+    gram = red[2] if r.gram is not None else None
     chain_stats = None
     if r.chain_stats is not None:
         width = max(shard_range(n_chains, k, world)[1] for k in range(world))
@@ -142,11 +341,11 @@ def imhk_sharded(compute: Callable, n_chains: int, n_steps: int, *, rank: int, w
         t = torch.from_numpy(buf)
         if device is not None:
             t = t.to(device)
-        if world > 1:
+        if collective_active():
             out = [torch.zeros_like(t) for _ in range(world)]
             dist.all_gather(out, t, group=group)  # the single gather
         else:
             out = [t]
         chain_stats = np.concatenate([o.cpu().numpy()[:shard_range(n_chains, k, world)[1]]
                                       for k, o in enumerate(out)])
-    return JobStats(int(s[0]), s[2:2 + d2], int(s[1]), gram, chain_stats)
+    return JobStats(int(s[0]), red[1], int(s[1]), gram, chain_stats)

@@ -27,3 +27,25 @@ def oracle_compute_factory(oracle, R, cp, B, sigma, seed, *, thin: int = 1, mode
         return ShardResult(int(st["accepts"].sum()), mom, kept.shape[0], gram, cs)
 
     return compute
+
+
+def oracle_advance_factory(oracle, R, cp, B, sigma, seed, first_chain, n_chains, *, mode: int = 0):
+    """CPU stand-in for `gpu_advance` (StreamingShard's per-rank compute): the
+    oracle's resumable IMHK chains, kept lattice points v = B z as a CPU tensor."""
+    import torch
+    d = R.shape[0]
+    st = {"state": None}
+
+    def advance(first_step, n_steps, acc, mom):
+        prev = st["state"]["accepts"].copy() if st["state"] is not None else np.zeros(n_chains, dtype=np.int64)
+        r = oracle.imhk(R, cp, B, sigma, n_chains, n_steps, seed=seed, first_chain=first_chain,
+                        first_step=first_step, state=st["state"], mode=mode, trace=True)  # resumes in place
+        tr = r.pop("trace")
+        st["state"] = r
+        acc += torch.from_numpy((r["accepts"] - prev).astype(np.int64))
+        kept = tr.reshape(-1, d).astype(np.int64)
+        mom += torch.from_numpy(np.concatenate([kept.sum(0), (kept * kept).sum(0)]))
+        return torch.from_numpy(tr.astype(np.float64) @ B.T)
+
+    advance.state = st
+    return advance

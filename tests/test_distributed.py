@@ -82,3 +82,65 @@ def test_gloo_world2_matches_single_process(oracle):
         import lgs_diag_oracle as O
         np.testing.assert_allclose(js.gelman_rubin(5), O.gelman_rubin([c for c in flat[:, :, 31].astype(float)]),
                                    rtol=1e-12)
+
+
+def _stream_worker(rank, world, port, out):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    for p in (os.path.join(repo, "lattice-gaussian-mcmc_amd"), os.path.join(repo, "oracle"), here):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    import lgs_oracle
+    from lgs_amd import distributed as D
+    from _oracle_shard import oracle_advance_factory
+    from conftest import golden_R, load_golden
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    D.init_process_group("gloo", 0, world, rank=rank)
+    out[rank] = _stream_stats(D, lgs_oracle, oracle_advance_factory, golden_R(load_golden("klein_ntru32.npz")),
+                              rank, world, torch)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _stream_stats(D, oracle, factory, RcpB, rank, world, torch):
+    """bench.py's timed path (StreamingShard: blocks of IMHK steps, lag sums, one
+    all-reduce) over this rank's contiguous shard of 6 chains, Wang-Ling weights."""
+    R, cp, B = RcpB
+    first, count = D.shard_range(6, rank, world)
+    adv = factory(oracle, R, cp, B, 165.7, 99, first, count, mode=oracle.IMHK_WANG_LING)
+    binv = np.linalg.inv(B)[B.shape[0] - 1]
+    sh = D.StreamingShard(adv, count, B.shape[0], binv_row=binv, device="cpu", lag_chains=6, lags=5)
+    sh.step(3)  # warm-up block, then fresh statistics as the bench does
+    sh.reduce()
+    sh.reset_stats()
+    for _ in range(3):
+        sh.step(4)
+    st = sh.reduce()
+    return {"accepts": st["accepts"].tolist(), "moments": st["moments"].tolist(),
+            "lag_z": [x.tolist() for x in st["lag_z"]], "lag_v": [x.tolist() for x in st["lag_v"]]}
+
+
+@pytest.mark.timeout(300)
+def test_streaming_shard_gloo_world2_matches_single_process(oracle):
+    """The bench's aggregation (StreamingShard + allreduce_parts) over gloo, world 2,
+    equals the single-process run over all chains.  The lag sums are over each
+    rank's first `lag_chains` chains, so the single-process reference sums the
+    same chains (lag_chains = 6: every chain of every shard)."""
+    import torch
+    from lgs_amd import distributed as D
+    from _oracle_shard import oracle_advance_factory
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_stream_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    g = golden_R(load_golden("klein_ntru32.npz"))
+    single = _stream_stats(D, oracle, oracle_advance_factory, g, 0, 1, torch)
+    for r in (0, 1):
+        assert out[r]["accepts"] == single["accepts"]
+        assert out[r]["moments"] == single["moments"]
+        assert out[r]["lag_z"] == single["lag_z"]          # int64: exact
+        np.testing.assert_allclose(np.array(out[r]["lag_v"][0]), np.array(single["lag_v"][0]), rtol=1e-13)
+        assert out[r]["lag_v"][1] == single["lag_v"][1]
+    assert 0 < single["accepts"][0] < 6 * 12  # Wang-Ling: some rejections
