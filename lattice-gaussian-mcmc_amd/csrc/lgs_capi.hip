@@ -103,6 +103,7 @@ struct lgs_ctx {
     // estimate from the basis, then twice the largest sum seen; a sample exceeding it
     // is replayed in the reference's order, so the cap only affects speed)
     double z1cap = 0.0, z1seen = 0.0;
+    unsigned int resolved_seen = 0;  // run_klein_store: the resolved word after the call's last launch
     DevBuf RD, RDOFF;             // int8-digit far field: R digit fragments, panel offsets
     bool has_rd = false, oz_off = false;  // oz_off: a |z| > 32767 was seen (sticky)
     DevBuf H16, F0;               // int8-digit far field scratch: coefficient history, tile-0 sums
@@ -128,8 +129,8 @@ struct lgs_ctx {
     int zint = 2;  // internal coefficient store width (bytes): 16-bit, sticky 32-bit on overflow; LGS_ZINT=4 forces 32-bit
     // timing
     bool timing = false;
-    double t_ms[6] = {0, 0, 0, 0, 0, 0};
-    int64_t t_n[6] = {0, 0, 0, 0, 0, 0};
+    double t_ms[7] = {0, 0, 0, 0, 0, 0, 0};
+    int64_t t_n[7] = {0, 0, 0, 0, 0, 0, 0};
     // diagnostics scratch (lgs_series_stats / lgs_gram / lgs_jump_distance / lgs_marginal_tvd)
     DevBuf dg_x, dg_y, dg_out, dg_a, dg_b, dg_c, dg_t;
     // decoding frame (lgs_set_decoder): Q of the QR and (B^{-1})^T, row-major d x d
@@ -205,6 +206,29 @@ int settle_bz(lgs_ctx* c) {
     return LGS_OK;
 }
 
+// flags buffer (device, 32 bytes): [0] kernel flag bits, [1] kFlagWordResolved
+// counter, [2..3] the largest sum |z_j| of a Klein launch (fp64 bits, atomicMax),
+// [4] lgs_imhk: some chain needs its initial draw, [5] lgs_imhk: the resolved
+// counter before the block's own Klein launch (a checkpoint taken by init_apply)
+using lgs::kFlagWordUninit;
+using lgs::kFlagWordCheckpoint;
+
+// Folds the counters of a finished stretch of launches into the context: the
+// resolved count, and the certificate's cap on sum |z_j| = twice the larger of the
+// largest sums of the last two stretches (the basis-derived bound of lgs_set_basis
+// only until a launch has been seen): a tight cap keeps the bound dmu small, and
+// one launch with outlying |z| no longer inflates it for good (a sum above the cap
+// only forces that sub-panel's verification).
+void fold_counters(lgs_ctx* c, const unsigned int* fw) {
+    c->n_resolved += fw[1];
+    double z1;
+    memcpy(&z1, fw + 2, sizeof(z1));
+    if (z1 > 0.0) {
+        c->z1cap = 2.0 * std::max(z1, c->z1seen);
+        c->z1seen = z1;
+    }
+}
+
 int finish(lgs_ctx* c) {  // sync, fold timers, report kernel flags
     int rc0 = settle_bz(c);
     if (rc0) return rc0;
@@ -218,21 +242,14 @@ int finish(lgs_ctx* c) {  // sync, fold timers, report kernel flags
         c->pool.push_back(t.b);
     }
     c->pending.clear();
-    unsigned int fw[4] = {0, 0, 0, 0};
+    unsigned int fw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIP_TRY(hipMemcpy(fw, c->flags.p, sizeof(fw), hipMemcpyDeviceToHost));
     const unsigned int f = fw[0];
-    if (fw[1]) {
-        c->n_resolved += fw[1];
-        fw[1] = 0;
-        HIP_TRY(hipMemcpy((unsigned int*)c->flags.p + 1, &fw[1], sizeof(unsigned int), hipMemcpyHostToDevice));
-    }
-    {
-        double z1;
-        memcpy(&z1, fw + 2, sizeof(z1));
-        if (z1 > c->z1seen) {
-            c->z1seen = z1;
-            c->z1cap = 2.0 * z1;
-        }
+    c->resolved_seen = 0;
+    if (fw[1] || fw[2] || fw[3]) {
+        fold_counters(c, fw);
+        const unsigned int zero[5] = {0, 0, 0, 0, 0};
+        HIP_TRY(hipMemcpy((unsigned int*)c->flags.p + 1, zero, sizeof(zero), hipMemcpyHostToDevice));
     }
     if (f & lgs::kFlagNonFinite)
         return fail(LGS_ERR_NONFINITE, "non-finite conditional mean (reference raises ValueError)");
@@ -241,12 +258,43 @@ int finish(lgs_ctx* c) {  // sync, fold timers, report kernel flags
     return LGS_OK;
 }
 
-// flags buffer: [0] kernel flag bits, [1] kFlagWordResolved counter, [2..3] the
-// largest sum |z_j| of a Klein launch (fp64 bits, atomicMax)
+// One synchronisation for a stretch of lgs_imhk launches enqueued without waiting
+// (a Klein launch and its dependants).  If the Klein launch overflowed its 16-bit
+// store / int16 history, or a carried-in state did not fit the 16-bit store
+// (kAbortMask), the dependants returned without touching the caller's state: the
+// attempt is discarded (its B z launches, its verification count beyond the
+// checkpoint, its |z| maximum), the context switches to the wider store / the fp64
+// far field, and redo is set.  Otherwise the usual finish().
+int finish_or_redo(lgs_ctx* c, bool oz_used, int& zb, bool& redo) {
+    redo = false;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    unsigned int fw[8];
+    HIP_TRY(hipMemcpy(fw, c->flags.p, sizeof(fw), hipMemcpyDeviceToHost));
+    if (!(fw[0] & lgs::kAbortMask)) return finish(c);
+    c->pending_i8.clear();
+    for (auto& t : c->pending) {  // the aborted attempt's timers are not kept
+        c->pool.push_back(t.a);
+        c->pool.push_back(t.b);
+    }
+    c->pending.clear();
+    c->n_fallback += 1;
+    c->n_resolved += fw[kFlagWordCheckpoint];
+    if (fw[0] & lgs::kFlagOverflow16) {
+        if (zb == 2) c->zint = 4;
+        if (oz_used) c->oz_off = true;
+    }
+    if (fw[0] & lgs::kFlagCarry16) c->zint = 4;
+    if (zb == 2) zb = c->zint;
+    HIP_TRY(hipMemsetAsync(c->flags.p, 0, 32, c->stream));
+    redo = true;
+    return LGS_OK;
+}
+
 int reset_flags(lgs_ctx* c) {
-    int rc = c->flags.reserve(16);
+    int rc = c->flags.reserve(32);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(c->flags.p, 0, 16, c->stream));
+    c->resolved_seen = 0;
+    HIP_TRY(hipMemsetAsync(c->flags.p, 0, 32, c->stream));
     return LGS_OK;
 }
 
@@ -286,7 +334,7 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
 // overrides (mfma64: fp64 MFMA far field).  Returns whether the int8-digit far
 // field was used.
 int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int zb, void* Z, bool& used_oz) {
-    Scope s(c, 0);
+    Scope s(c, a.gate ? 6 : 0);  // gated launches (lgs_imhk's initial draws) on their own timer
     static const char* force = getenv("LGS_KERNEL");
     int kernel = lgs::kKernelValu;
     used_oz = false;
@@ -320,32 +368,43 @@ int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int zb, void* 
 // Klein launch into an internal coefficient store of width zb.  A coefficient
 // beyond int16 (a 16-bit store, or the int16 history of the int8-digit far field)
 // redoes the launch -- same counters, same samples -- at 32 bits / with the fp64
-// far field, and the context keeps that choice.
-int run_klein_store(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int& zb, void* Z) {
+// far field, and the context keeps that choice.  deferred (lgs_imhk): no wait
+// here; the caller's single synchronisation (finish_or_redo) makes that check.
+int run_klein_store(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int& zb, void* Z, bool deferred,
+                    bool* oz_out = nullptr) {
     bool oz = false;
     int rc = run_klein(c, a, exact, wl, zb, Z, oz);
-    if (rc || (zb != 2 && !oz)) return rc;
+    if (oz_out) *oz_out = oz;
+    if (oz) {
+        c->hist.Z = Z;
+        c->hist.lanes = (a.n + 63) / 64 * 64;
+        c->hist.cols = a.n;
+    }
+    if (rc || deferred || (zb != 2 && !oz)) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
-    unsigned int f = 0;
-    HIP_TRY(hipMemcpy(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost));
-    if (!(f & lgs::kFlagOverflow16)) {
-        if (oz) {
-            c->hist.Z = Z;
-            c->hist.lanes = (a.n + 63) / 64 * 64;
-            c->hist.cols = a.n;
-        }
+    unsigned int f[2] = {0, 0};
+    HIP_TRY(hipMemcpy(f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost));
+    if (!(f[0] & lgs::kFlagOverflow16)) {
+        c->resolved_seen = f[1];  // the count up to and including this launch
         return LGS_OK;
     }
-    f &= ~lgs::kFlagOverflow16;
+    // discard this launch's verification count: keep what earlier launches of the
+    // call had counted (folded into the context now, the word restarts at 0)
+    c->n_resolved += c->resolved_seen;
+    c->resolved_seen = 0;
+    f[0] &= ~lgs::kFlagOverflow16;
+    f[1] = 0;
     c->n_fallback += 1;
-    HIP_TRY(hipMemcpy(c->flags.p, &f, sizeof(f), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemsetAsync((unsigned int*)c->flags.p + lgs::kFlagWordResolved, 0, sizeof(unsigned int), c->stream));
+    HIP_TRY(hipMemcpy(c->flags.p, f, sizeof(f), hipMemcpyHostToDevice));
     if (zb == 2) {
         c->zint = 4;
         zb = 4;
     }
     if (oz) c->oz_off = true;
-    return run_klein(c, a, exact, wl, zb, Z, oz);
+    c->hist.Z = nullptr;
+    rc = run_klein(c, a, exact, wl, zb, Z, oz);
+    if (oz_out) *oz_out = oz;
+    return rc;
 }
 
 int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
@@ -361,11 +420,16 @@ int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
 // then a valid source of the digits for the columns that launch wrote).
 int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
            int64_t rb = 0, int64_t rstride = 0, int64_t roff = 0, const int64_t* sel = nullptr,
-           bool after_klein = false) {
+           bool after_klein = false, const unsigned int* abort = nullptr) {
     if (!c->has_B) return fail(LGS_ERR_STATE, "lattice points need B (lgs_set_basis B != NULL)");
     BzCall b{Z, zb, ldz, n, V, rb > 0 ? rb : n, rstride, roff, sel};
     static const bool force64 = getenv("LGS_BZ_FP64") && atoi(getenv("LGS_BZ_FP64")) == 1;
-    if (!c->has_Bi8 || force64) return run_bz_fp64(c, b);
+    if (!c->has_Bi8 || force64) {
+        Scope s(c, 1);
+        HIP_TRY(lgs::launch::bz(b.Z, b.zb, b.ldz, b.sel, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
+                                b.rstride, b.roff, c->stream, abort));
+        return LGS_OK;
+    }
     Scope s(c, 1);
     const int8_t* hi = c->Bd.as<int8_t>();
     const int8_t* lo = hi + (size_t)c->bd_rows * c->bd_cols;
@@ -373,7 +437,7 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
                                (int)c->bd_cols, (int)c->d, n, V, c->d, b.rb,
                                b.rstride, b.roff, c->flags.as<unsigned int>(),
                                after_klein && c->hist.Z == Z && Z ? c->H16.as<int16_t>() : nullptr, c->hist.lanes,
-                               c->hist.cols, c->stream));
+                               c->hist.cols, c->stream, abort));
     c->pending_i8.push_back(b);
     return LGS_OK;
 }
@@ -786,7 +850,7 @@ int lgs_klein(lgs_ctx* c, uint64_t seed, uint64_t first, int64_t n, void* z_out,
             a.ldz = m;
         }
         a.LW = logw_out ? (dev ? logw_out + off : c->LW.as<double>()) : nullptr;
-        if ((rc = run_klein_store(c, a, exact, wl, zb, Zp))) return rc;
+        if ((rc = run_klein_store(c, a, exact, wl, zb, Zp, false))) return rc;
         if (z_out && !direct) {
             if (cm) {  // coordinate-major output through host pointers (zb == ob)
                 for (int64_t i = 0; i < d; ++i)
@@ -949,11 +1013,7 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
     double* lws = logw_state;
     int32_t* init = state_init;
     int64_t* acc = accepts;
-    std::vector<int32_t> h_init(nc);
-    if (dev) {
-        HIP_TRY(hipMemcpyAsync(h_init.data(), state_init, nc * 4, hipMemcpyDeviceToHost, c->stream));
-    } else {
-        memcpy(h_init.data(), state_init, nc * 4);
+    if (!dev) {
         if ((rc = c->stage_a.reserve((size_t)nc * d * ob)) || (rc = c->stage_b.reserve((size_t)nc * 8)) ||
             (rc = c->stage_c.reserve((size_t)nc * 4)) || (rc = c->stage_d.reserve((size_t)nc * 8)))
             return rc;
@@ -986,56 +1046,40 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
             HIP_TRY(hipMemcpyAsync(mom, moments, (size_t)2 * d * 8, hipMemcpyHostToDevice, c->stream));
         }
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    unsigned int* fl = c->flags.as<unsigned int>();
 
-    // ---- initial draws (counter step 0) for uninitialised chains (imhk.py:126-139)
-    bool any_uninit = false;
-    for (int64_t i = 0; i < nc; ++i) any_uninit |= (h_init[i] == 0);
-    if (any_uninit) {
-        lgs::KleinArgs a = base_args(c, seed);
-        a.counter_mode = 1;
-        a.chain0 = (uint32_t)first_chain;
-        a.step0 = 0;
-        a.nt = 1;
-        a.n = nc;
-        a.ldz = nc;
-        a.LW = c->LW.as<double>();
-        if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p))) return rc;
-        std::vector<int64_t> s(nc);
-        for (int64_t i = 0; i < nc; ++i) s[i] = h_init[i] ? -1 : i;
-        HIP_TRY(hipMemcpyAsync(c->sel.p, s.data(), nc * 8, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, nc, c->sel.as<int64_t>(), nc, 1, zs, ob, cm, nc,
-                                      (int)d, zs, cm, c->stream));
-        std::vector<double> h_lw(nc), cur(nc);
-        HIP_TRY(hipMemcpyAsync(h_lw.data(), c->LW.p, nc * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(cur.data(), lws, nc * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        for (int64_t i = 0; i < nc; ++i)
-            if (!h_init[i]) {
-                cur[i] = h_lw[i];
-                h_init[i] = 1;
-            }
-        HIP_TRY(hipMemcpyAsync(lws, cur.data(), nc * 8, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(init, h_init.data(), nc * 4, hipMemcpyHostToDevice, c->stream));
-    }
-
-    // ---- a 16-bit proposal store receives the chain states through carry_cols:
-    // states that do not fit (caller-supplied ones) switch this context to 32 bits
-    if (zb == 2 && carry && n_steps > 0) {
-        HIP_TRY(lgs::launch::check_range16(zs, ob, nc * d, c->flags.as<unsigned int>(), c->stream));
-        unsigned int f = 0;
-        HIP_TRY(hipMemcpyAsync(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        if (f & lgs::kFlagOverflow16) {
-            f &= ~lgs::kFlagOverflow16;
-            HIP_TRY(hipMemcpy(c->flags.p, &f, sizeof(f), hipMemcpyHostToDevice));
-            c->zint = 4;
-            zb = 4;
+    // Every launch below is enqueued without a host round trip; the call waits once
+    // per block (finish_or_redo).  A block whose Klein launch (or the chain states
+    // carried into a 16-bit store) overflowed has its state-modifying dependants
+    // skipped on the device (kAbortMask) and is redone at the wider width.
+    for (int64_t t0 = 0; t0 < n_steps || t0 == 0;) {
+        bool oz_used = false;
+        // ---- initial draws (counter step 0) of uninitialised chains (imhk.py:126-139),
+        // decided on the device: the Klein launch and its application are gated by
+        // "some chain has init == 0" (block 0 of the call only)
+        if (t0 == 0) {
+            HIP_TRY(lgs::launch::uninit_scan(init, nc, fl + kFlagWordUninit, c->stream));
+            lgs::KleinArgs a = base_args(c, seed);
+            a.counter_mode = 1;
+            a.chain0 = (uint32_t)first_chain;
+            a.step0 = 0;
+            a.nt = 1;
+            a.n = nc;
+            a.ldz = nc;
+            a.LW = c->LW.as<double>();
+            a.gate = fl + kFlagWordUninit;
+            bool oz0 = false;
+            if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p, true, &oz0))) return rc;
+            oz_used |= oz0;
+            HIP_TRY(lgs::launch::init_apply(c->Z.p, zb, init, nc, (int)d, c->LW.as<double>(), zs, ob, cm, lws,
+                                            fl, c->stream));
         }
-    }
-
-    // ---- blocks
-    for (int64_t t0 = 0; t0 < n_steps; t0 += T) {
+        if (n_steps == 0) {
+            bool redo = false;
+            if ((rc = finish_or_redo(c, oz_used, zb, redo))) return rc;
+            if (redo) continue;
+            break;
+        }
         const int64_t Tb = std::min<int64_t>(T, n_steps - t0);
         const int64_t npb = nc * Tb;
         const int64_t first_keep = t0 / thin;  // t0 is a multiple of thin
@@ -1049,9 +1093,12 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
         a.n = npb;
         a.ldz = ldzb;
         a.LW = c->LW.as<double>();
-        if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p))) return rc;
+        bool ozb = false;
+        if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p, true, &ozb))) return rc;
+        oz_used |= ozb;
+        // chain states carried into the block's store (a state beyond 16 bits flags kFlagCarry16)
         if (carry && kb > 0)
-            HIP_TRY(lgs::launch::carry_cols(zs, ob, cm, nc, (int)d, c->Z.p, zb, ldzb, npb, c->stream));
+            HIP_TRY(lgs::launch::carry_cols(zs, ob, cm, nc, (int)d, c->Z.p, zb, ldzb, npb, c->stream, fl));
         if (moments) HIP_TRY(hipMemsetAsync(c->cnt.p, 0, (size_t)npb * 4, c->stream));
         lgs::AcceptArgs aa{};
         aa.nc = nc;
@@ -1073,6 +1120,7 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
         aa.lw_ld = n_keep;
         aa.acc_step = accs ? accs + t0 : nullptr;
         aa.acc_ld = n_steps;
+        aa.abort = fl;
         {
             Scope s(c, 2);
             HIP_TRY(lgs::launch::accept(aa, c->stream));
@@ -1083,25 +1131,26 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
         if (moments) {
             Scope s(c, 3);
             // carried-in states first: the fused pass overwrites z_state
-            HIP_TRY(lgs::launch::moments_carry(zs, ob, cm, nc, (int)d, c->ccnt.as<int32_t>(), mom, c->stream));
+            HIP_TRY(lgs::launch::moments_carry(zs, ob, cm, nc, (int)d, c->ccnt.as<int32_t>(), mom, c->stream, fl));
             HIP_TRY(lgs::launch::moments_final(c->Z.p, zb, ldzb, c->cnt.as<int32_t>(), npb, Tb,
                                                fuse_final ? c->fsel.as<int64_t>() : nullptr, (int)d, mom, zs,
-                                               ob, cm, nc, c->stream));
+                                               ob, cm, nc, c->stream, fl));
         }
         if ((z_samples || v_samples) && kb > 0) {
             // kept states q = chain*kb + k, gathered coordinate-major (d x nq); chain-major
-            // proposal order makes this a near-contiguous copy
+            // proposal order makes this a near-contiguous copy (outputs only: an aborted
+            // attempt's values are overwritten by the redo)
             const int64_t nq = nc * kb;
             if (v_samples) {  // rows (chain, first_keep + k) of the n_chains x n_keep x d output,
                               // read straight from the proposal store through the selections
                 if ((rc = run_bz(c, c->Z.p, zb, ldzb, nq, v_samples, kb, n_keep, first_keep,
-                                 c->sel.as<int64_t>(), true)))
+                                 c->sel.as<int64_t>(), true, fl)))
                     return rc;
             }
             if (z_samples) {
                 if ((rc = c->stage_f.reserve((size_t)nq * d * ob))) return rc;
                 HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, ldzb, c->sel.as<int64_t>(), nq, kb, zs, ob, cm,
-                                              nc, (int)d, c->stage_f.p, 1, c->stream));
+                                              nc, (int)d, c->stage_f.p, 1, c->stream, fl));
                 if ((rc = c->stage_g.reserve((size_t)nq * d * ob))) return rc;
                 HIP_TRY(lgs::launch::transpose_out(c->stage_f.p, ob, nq, nq, (int)d, c->stage_g.p,
                                                    ob, c->stream));
@@ -1113,8 +1162,11 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
         // chain states after the block (in place; carried chains keep their row)
         if (!fuse_final)
             HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, ldzb, c->fsel.as<int64_t>(), nc, 1, zs, ob, cm, nc,
-                                          (int)d, zs, cm, c->stream));
-        if ((rc = finish(c))) return rc;
+                                          (int)d, zs, cm, c->stream, fl));
+        bool redo = false;
+        if ((rc = finish_or_redo(c, oz_used, zb, redo))) return rc;
+        if (redo) continue;  // same block again (block 0: its initial draws too)
+        t0 += T;
     }
     if (!dev) {
         HIP_TRY(hipMemcpyAsync(z_state, zs, (size_t)nc * d * ob, hipMemcpyDeviceToHost, c->stream));
@@ -1127,8 +1179,9 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
             HIP_TRY(hipMemcpyAsync(logw_samples, lwk, (size_t)nc * n_keep * 8, hipMemcpyDeviceToHost, c->stream));
         if (accepted && n_steps > 0)
             HIP_TRY(hipMemcpyAsync(accepted, accs, (size_t)nc * n_steps, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
     }
-    return finish(c);
+    return LGS_OK;
 }
 
 int lgs_sample_z(lgs_ctx* c, int64_t n, const double* mu, const double* sigma, const double* u,
@@ -1169,7 +1222,7 @@ int lgs_timing_enable(lgs_ctx* c, int enable) {
     int rc = check_ctx(c, false);
     if (rc) return rc;
     c->timing = enable != 0;
-    for (int k = 0; k < 6; ++k) {
+    for (int k = 0; k < 7; ++k) {
         c->t_ms[k] = 0;
         c->t_n[k] = 0;
     }
@@ -1178,7 +1231,7 @@ int lgs_timing_enable(lgs_ctx* c, int enable) {
 
 int lgs_timing_get(lgs_ctx* c, int kernel, double* ms, int64_t* n) {
     if (!c) return fail(LGS_ERR_INVALID, "null context");
-    if (kernel < 0 || kernel > 5) return fail(LGS_ERR_INVALID, "kernel id 0..5");
+    if (kernel < 0 || kernel > 6) return fail(LGS_ERR_INVALID, "kernel id 0..6");
     if (ms) *ms = c->t_ms[kernel];
     if (n) *n = c->t_n[kernel];
     return LGS_OK;

@@ -791,24 +791,47 @@ __device__ __forceinline__ double poly_estrin(const double (&c)[N], double x) {
     return p[0];
 }
 
+// Polynomial coefficients of the capped decision (below), in constant memory and
+// read through a pointer the compiler cannot prove invariant: inside the rolled
+// coordinate loop of klein_mfma_kernel they are then scalar loads per coordinate
+// instead of ~36 fp64 constants hoisted into VGPRs for the whole loop (with a copy
+// before every fmac).
+//   [0, 11)  erf(y)/y as a polynomial in z = y^2 on [0, 1] (Chebyshev fit; 4.5e-15 rel. of libm)
+//   [11, 23) e^{-z} on [0, 1] (2.6e-15 rel.)
+//   [23, 36) erfinv(v) = v R(v^2), |v| <= 0.849 (relative error 3e-8)
+__device__ __constant__ double kCapCoef[36] = {
+    1.1283791670955137, -0.3761263890318955, 0.11283791670856351, -0.0268661706101513, 0.005223977272142491,
+    -0.000854830863419428, 0.00012054761075042809, -1.491439328403532e-05, 1.6319831426837587e-06,
+    -1.5234934784514681e-07, 9.527703833862884e-09,
+    0.9999999999999993, -0.9999999999999447, 0.4999999999972167, -0.16666666661556404, 0.04166666619559115,
+    -0.008333330756823971, 0.0013888798425041814, -0.00019839153700921557, 2.4768196009077585e-05,
+    -2.72048331078728e-06, 2.5149219471527703e-07, -1.5159419884388667e-08,
+    0.8862269447150851, 0.23200895985592382, 0.1278390124627034, 0.07920907048159789, 0.16780265291085433,
+    -0.8188084361376584, 4.787814391235978, -17.187235185827564, 42.14891487326897, -68.64189227692192,
+    71.76515059941498, -43.593212219926436, 11.853485934431038};
+constexpr int kCapE = 0, kCapG = 11, kCapRI = 23;
+__device__ __forceinline__ cdptr cap_coef() {
+    cdptr p = (cdptr)kCapCoef;
+    asm volatile("" : "+s"(p));
+    return p;
+}
+template <int N>
+__device__ __forceinline__ double poly_estrin_p(cdptr cf, double x) {
+    double c[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) c[k] = cf[k];
+    return poly_estrin(c, x);
+}
+
 // C(k) - base of a capped window with sigma >= 360 (Euler-Maclaurin with 3 terms,
 // as em_P_tab<3>), erf / exp from fitted polynomials in Estrin form; fk = f(k).
-__device__ __forceinline__ double capped_C(double kd, double m, double sig, double is, double base, double& fk) {
-    // erf(y)/y and e^{-z} as polynomials in z = y^2 on [0, 1] (Chebyshev fits;
-    // within 4.5e-15 and 2.6e-15 relative of libm), 11 and 12 terms
-    constexpr double E[11] = {1.1283791670955137, -0.3761263890318955, 0.11283791670856351,
-                              -0.0268661706101513, 0.005223977272142491, -0.000854830863419428,
-                              0.00012054761075042809, -1.491439328403532e-05, 1.6319831426837587e-06,
-                              -1.5234934784514681e-07, 9.527703833862884e-09};
-    constexpr double G[12] = {0.9999999999999993, -0.9999999999999447, 0.4999999999972167,
-                              -0.16666666661556404, 0.04166666619559115, -0.008333330756823971,
-                              0.0013888798425041814, -0.00019839153700921557, 2.4768196009077585e-05,
-                              -2.72048331078728e-06, 2.5149219471527703e-07, -1.5159419884388667e-08};
+__device__ __forceinline__ double capped_C(double kd, double m, double sig, double is, double base, double& fk,
+                                           cdptr cf) {
     const double t = (kd - m) * is;
     const double t2 = t * t;
     const double z = 0.5 * t2;  // y^2, y = t / sqrt 2
-    const double erf_y = (t * kInvSqrt2) * poly_estrin(E, z);
-    fk = poly_estrin(G, z);
+    const double erf_y = (t * kInvSqrt2) * poly_estrin_p<11>(cf + kCapE, z);
+    fk = poly_estrin_p<12>(cf + kCapG, z);
     // sum_m c_m He_{2m+1}(t) / sigma^{2m+1}: He1 = t, He3 = t^3 - 3t, He5 = t^5 - 10t^3 + 15t
     const double is2 = is * is;
     const double he3 = t * (t2 - 3.0);
@@ -839,16 +862,12 @@ __device__ __forceinline__ double sample_z_capped(double mu, double u, const QHe
     const double S = poly_estrin(cS, m), base = poly_estrin(cB, m);
     const double target = u * S;
     // continuous quantile x = m + sigma sqrt(2) erfinv(v): erfinv(v) = v R(v^2)
-    constexpr double RI[13] = {0.8862269447150851, 0.23200895985592382, 0.1278390124627034,
-                               0.07920907048159789, 0.16780265291085433, -0.8188084361376584,
-                               4.787814391235978, -17.187235185827564, 42.14891487326897,
-                               -68.64189227692192, 71.76515059941498, -43.593212219926436,
-                               11.853485934431038};
+    const cdptr cf = cap_coef();
     const double v = fmin(fmax((target + base) * h.v[4], -0.8485), 0.8485);
-    const double xg = fma(h.v[5] * v, poly_estrin(RI, v * v), m);
+    const double xg = fma(h.v[5] * v, poly_estrin_p<13>(cf + kCapRI, v * v), m);
     double kd = fmin(fmax(ceil(xg - 0.5), -500.0), 500.0);
     double fk;
-    double Ck = capped_C(kd, m, sig, is, base, fk);
+    double Ck = capped_C(kd, m, sig, is, base, fk, cf);
     if (__builtin_amdgcn_ballot_w64(!(Ck > target) || (kd > -500.0 && Ck - fk > target)) != 0) {
 #pragma nounroll
         for (int it = 0; it < 64 && Ck <= target && kd < 500.0; ++it) {  // move up

@@ -10,9 +10,17 @@ constexpr unsigned int kFlagNonFinite = 1u;  // a conditional mean was NaN/inf
 constexpr unsigned int kFlagOverflow = 2u;   // |z| >= 2^31 with an int32 store
 constexpr unsigned int kFlagI8Range = 4u;    // |z| > 32639: int8-digit B z must be redone in fp64
 constexpr unsigned int kFlagOverflow16 = 8u; // |z| > 32767 in a 16-bit internal store
+constexpr unsigned int kFlagCarry16 = 16u;   // a chain state carried into a 16-bit store does not fit
+// lgs_imhk enqueues a block's Klein launch and its dependants without waiting: the
+// dependants that modify caller state (acceptance, moments, state gathers, initial
+// draws) return immediately when the launch set one of these, and the block is
+// redone at the wider width after the call's single synchronisation
+constexpr unsigned int kAbortMask = kFlagOverflow16 | kFlagCarry16;
 // flags[1] of a launch: coordinates whose decision at the blocked-order mean could
 // not be certified and was redone at the reference-order mean (lgs_device.h)
 constexpr int kFlagWordResolved = 1;
+constexpr int kFlagWordUninit = 4;      // lgs_imhk: some chain needs its initial draw
+constexpr int kFlagWordCheckpoint = 5;  // lgs_imhk: resolved count before the block's Klein launch
 
 constexpr int kErfTabLast = 512;
 constexpr int kCoefStride = 18;  // doubles per grid point of the coefficient table (lgs_device.h CoefTab)  // SampleZ erf/exp table: y_j = j/64, j = 0..kErfTabLast (y <= 8)
@@ -110,6 +118,8 @@ struct KleinArgs {
     int h16_shift;           // (16 - d % 16) % 16
     int64_t h16_lanes;       // lanes per 16-coordinate block (>= n)
     const double* rx;    // per 32-row panel: 16x16 block R[p_hi-32.., p_hi-16..] as MFMA A fragments
+    const unsigned int* gate;  // nullable: when *gate == 0 every block returns at once (initial draws
+                               // of lgs_imhk when no chain needs one, decided on the device)
 };
 
 struct AcceptArgs {
@@ -132,6 +142,7 @@ struct AcceptArgs {
     int64_t lw_ld;
     uint8_t* acc_step;   // nullable: 1 where step t of chain c accepted, at acc_step[c * acc_ld + t]
     int64_t acc_ld;
+    const unsigned int* abort;  // nullable: return at once when *abort & kAbortMask
 };
 
 // Per-series statistics (lgs_diag.hip series_stats_kernel).  Series s starts at
@@ -197,14 +208,24 @@ hipError_t samplez_probe(const double* mu, const double* sig, const double* u, i
 hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, int zb, double* out,
                        hipStream_t st);
 // moments of the proposal store + (fsel non-null) the chains' final states into zs
+// abort (nullable) below: the kernel returns at once when *abort & kAbortMask
 hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int64_t T,
                          const int64_t* fsel, int d, unsigned long long* mom, void* zs, int ob,
-                         int zs_cm, int64_t nc, hipStream_t st);
+                         int zs_cm, int64_t nc, hipStream_t st, const unsigned int* abort = nullptr);
 hipError_t moments_carry(const void* zs, int zb, int coord_major, int64_t nc, int d,
-                         const int32_t* cc, unsigned long long* mom, hipStream_t st);
+                         const int32_t* cc, unsigned long long* mom, hipStream_t st,
+                         const unsigned int* abort = nullptr);
 hipError_t gather_z(const void* Z, int zb, int64_t ldz, const int64_t* sel, int64_t nq,
                     int64_t q_per_chain, const void* zs, int ob, int zs_coord_major, int64_t nc,
-                    int d, void* out, int out_coord_major, hipStream_t st);
+                    int d, void* out, int out_coord_major, hipStream_t st,
+                    const unsigned int* abort = nullptr);
+// initial IMHK draws decided on the device: uninit_scan sets *any when some
+// init[c] == 0; init_apply (gated by *any, abortable) gives each such chain the
+// proposal of column c of Z (ld nc) and its log weight LW[c], and marks it initialised
+hipError_t uninit_scan(const int32_t* init, int64_t nc, unsigned int* any, hipStream_t st);
+// (flags: the context's flag words; init_apply also checkpoints the resolved count)
+hipError_t init_apply(const void* Z, int zb, int32_t* init, int64_t nc, int d, const double* LW, void* zs,
+                      int ob, int zs_cm, double* lws, unsigned int* flags, hipStream_t st);
 hipError_t transpose_out(const void* Z, int zb, int64_t ldz, int64_t n, int d, void* out, int ob,
                          hipStream_t st);
 hipError_t to_coord_major(const void* in, int ib, int64_t n, int d, void* Z, int zb, int64_t ldz,
@@ -212,12 +233,12 @@ hipError_t to_coord_major(const void* in, int ib, int64_t n, int d, void* Z, int
 // V row of sample s: (s / rb) * rstride + roff + s % rb (rb = n, rstride = roff = 0: row s)
 hipError_t bz(const void* Z, int zb, int64_t ldz, const int64_t* sel, const double* BT, int d,
               int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
-              hipStream_t st);
+              hipStream_t st, const unsigned int* abort = nullptr);
 hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const int* kchunk,
                  const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
-                 hipStream_t st);
+                 hipStream_t st, const unsigned int* abort = nullptr);
 // ---- decoding
 // V (row-major n x d) = rows s: sum_c MT[c][r] X[c][s], X coordinate-major fp64 (fp64 MFMA)
 hipError_t gemm_f64(const double* X, int64_t ldx, const double* MT, int d, int64_t n, double* V,
@@ -228,7 +249,8 @@ hipError_t nearest_plane(int d, int64_t n, int panel, const double* RP, const do
 hipError_t round_coeffs(const double* W, int64_t ldw, int d, int64_t n, int zb, void* Z, int64_t ldz,
                         unsigned int* flags, hipStream_t st);
 hipError_t check_range16(const void* zs, int ob, int64_t count, unsigned int* flags, hipStream_t st);
+// (a value that does not fit a 16-bit store sets kFlagCarry16 in *flags)
 hipError_t carry_cols(const void* zs, int ob, int zs_coord_major, int64_t nc, int d, void* Z, int zb,
-                      int64_t ldz, int64_t col0, hipStream_t st);
+                      int64_t ldz, int64_t col0, hipStream_t st, unsigned int* flags = nullptr);
 }  // namespace launch
 }  // namespace lgs

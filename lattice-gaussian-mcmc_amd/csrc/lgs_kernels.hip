@@ -21,6 +21,11 @@
 #include <type_traits>
 #include <stdint.h>
 
+// The rolled near field (default) decides the capped kind inline (one copy in the
+// loop body); the unrolled one (LGS_NEAR_UNROLLED) calls it as a leaf.
+#if !defined(LGS_NEAR_UNROLLED) && !defined(LGS_CAPPED_CALL) && !defined(LGS_CAPPED_INLINE)
+#define LGS_CAPPED_INLINE
+#endif
 #include "lgs_device.h"
 #include "lgs_kernels.h"
 
@@ -484,6 +489,7 @@ template <typename ZT, bool WL>
 __global__ __launch_bounds__(256) void klein_exact_kernel(const KleinArgs a,
                                                           const double* __restrict__ R,
                                                           ZT* __restrict__ Z) {
+    if (a.gate && *a.gate == 0u) return;  // whole grid: nothing to draw
     __shared__ double tab_lds[2 * (kErfTabLast + 1)];
     const lds_cdptr etab_s = stage_etab(tab_lds, a.etab);
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -519,6 +525,7 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
                                                           const double* __restrict__ RP,
                                                           const double* __restrict__ RC,
                                                           ZT* __restrict__ Z) {
+    if (a.gate && *a.gate == 0u) return;  // whole grid: nothing to draw
     __shared__ double tab_lds[2 * (kErfTabLast + 1)];
     const lds_cdptr etab_s = stage_etab(tab_lds, a.etab);
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -912,6 +919,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                                                             const double* __restrict__ RP,
                                                             const double* __restrict__ RC,
                                                             ZT* __restrict__ Z) {
+    if (a.gate && *a.gate == 0u) return;  // whole grid: nothing to draw
     constexpr int NT = PB / 16, LDF = 65;  // LDS tile pitch (doubles): conflict-free row reads
     __shared__ double Fl[4][16 * LDF];
     // OZ: the erf table stays in global memory (L1-resident lookups measured as fast
@@ -1106,6 +1114,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
             // still in flight at a SampleZ call would be waited for at the callee's
             // entry (the calling convention starts with s_waitcnt 0).
             bool pnz = false;  // (OZ) a nonzero coefficient in this panel, this lane
+#ifdef LGS_NEAR_UNROLLED  // the round-2 near field: 16 steps unrolled, SampleZ as leaf calls
             auto near16 = [&](int rows16, int top) __attribute__((always_inline)) {
                 using ZH = std::conditional_t<sizeof(ZT) == 8, double, int>;
                 ZH zh[16];
@@ -1219,6 +1228,96 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     if constexpr (OZ) pnz |= vo.nz != 0;
                 }
             };
+#endif
+            // Rolled near field (default): one loop iteration per coordinate with the
+            // decision inline -- no call in the hot path, so no SGPR spill / restore
+            // around it, no wait-for-everything at a callee's entry, and the record
+            // loads of the next steps can be scheduled under the current decision.
+            // The running sums shift by one each step as part of the 15 FMAs
+            // (acc[k + 1] = acc[k] + R[i-15+k][i] z_i, written in descending k, so in
+            // place): acc[15] is always the current coordinate's sum.  z is stored per
+            // step; the int16 history is packed into 8 registers (step s at position
+            // 15 - s) and written as two 16-byte stores at the end.
+            auto near16r = [&](int rows16, int top) __attribute__((always_inline)) {
+                cert_lds[1][threadIdx.x] = cert_lds[0][threadIdx.x];  // sum |z_j| before the sub-panel
+                cert_lds[2][threadIdx.x] = lw;
+                double z1e = cert_lds[0][threadIdx.x];
+                const bool hblock = OZ && rows16 == 16;
+                unsigned int hp[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) hp[j] = 0u;
+                int flm = 0;
+                typedef double d2v __attribute__((ext_vector_type(2)));
+#pragma nounroll
+                for (int s = 0; s < rows16; ++s) {
+                    const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
+                    const lds_cdptr rec = (lds_cdptr)rec_lds + (i - (p_hi - 32)) * kRecStride;
+                    static_assert(kSzCa == 21 && kSzCb == 22 && kRecCp == 23 && kRecIrii == 24, "record layout");
+                    const d2v r22 = ((const __attribute__((address_space(3))) d2v*)rec)[11];
+                    const d2v r24 = ((const __attribute__((address_space(3))) d2v*)rec)[12];
+                    const double rca = rec[kSzCa];
+                    const double mu = (r22[1] - acc[15]) * r24[0];
+                    LGS_DC_T(t_sz0);
+                    bool un;
+                    const double zi = decide_coord_rec<WL, true, LIBM>(a, i, mu, rec, rs, lw, flags, etab_s,
+                                                                       cert_dmu(rca, r22[0], a.z1cap, mu), un);
+                    flm |= un ? (1 << s) : 0;
+#ifdef LGS_DIAG_CYCLES
+                    {
+                        LGS_DC_T(t_sz1);
+                        const int kind = (int)rec[2] & 7;
+                        LGS_DC_ADD(3 + kind, t_sz1 - t_sz0);
+                        LGS_DC_ADD(8 + kind, 1);
+                    }
+#endif
+                    if constexpr (sizeof(ZT) == 8) {
+                        Z[(size_t)i * ldz + p] = (ZT)(int64_t)zi;
+                    } else {
+                        if (sizeof(ZT) == 4 && !(zi <= 2147483647.0 && zi >= -2147483648.0)) flags |= kFlagOverflow;
+                        if (sizeof(ZT) == 2 && !(zi <= 32767.0 && zi >= -32768.0)) flags |= kFlagOverflow16;
+                        Z[(size_t)i * ldz + p] = (ZT)(int)fmin(fmax(zi, -2147483648.0), 2147483647.0);
+                    }
+                    if constexpr (OZ) {
+                        if (!(zi <= 32639.0 && zi >= -32767.0)) flags |= kFlagOverflow16;
+                        // int16 history value (z + 128, clamped to the far field's digit range)
+                        const unsigned int hv = (unsigned int)((int)(fmin(fmax(zi, -32767.0), 32639.0) + 128.0)) & 0xffffu;
+                        if (hblock) {
+#pragma unroll
+                            for (int j = 7; j >= 1; --j) hp[j] = __builtin_amdgcn_alignbit(hp[j], hp[j - 1], 16);
+                            hp[0] = (hp[0] << 16) | hv;
+                        } else {
+                            const int ih = i + a.h16_shift;
+                            a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] = (int16_t)hv;
+                        }
+                        pnz |= zi != 0.0;
+                    }
+                    z1e += fabs(zi);
+                    const lds_cdptr rc = rec + kRecRs;
+#pragma unroll
+                    for (int k = 14; k >= 0; --k) acc[k + 1] = fma(rc[14 - k], zi, acc[k]);
+                    acc[0] = 0.0;
+                }
+                if constexpr (OZ) {
+                    if (hblock) {
+                        v4u_t* hp4 = (v4u_t*)(a.h16 + ((size_t)((top - 16 + a.h16_shift) >> 4) * a.h16_lanes + p) * 16);
+                        hp4[0] = (v4u_t){hp[0], hp[1], hp[2], hp[3]};
+                        hp4[1] = (v4u_t){hp[4], hp[5], hp[6], hp[7]};
+                    }
+                }
+                // the certificate used sum_{j>i} |z_j| <= z1cap: verify it (the sum at the
+                // sub-panel's end bounds every coordinate's) -- else replay
+                cert_lds[0][threadIdx.x] = z1e;
+                const int fl = flm | (z1e > a.z1cap ? (1 << 16) : 0);
+                if (__builtin_amdgcn_ballot_w64(fl != 0) != 0) {  // rare: verify / replay (whole wave)
+                    const int w64 = threadIdx.x & ~63;
+                    const VerifyOut vo = verify_subpanel<WL, OZ>(kernel_args(), Z, ldz, p0, top, rows16, fl, lw,
+                                                                 rs.step, rs.chain, &cert_lds[0][w64],
+                                                                 &cert_lds[1][w64], &cert_lds[2][w64], flags);
+                    lw = vo.lw;
+                    flags = vo.flags;
+                    if constexpr (OZ) pnz |= vo.nz != 0;
+                }
+            };
             // one copy of the 16-step near field for both sub-panels (a second inlined
             // copy doubles the hot loop's code beyond the instruction cache)
 #pragma nounroll
@@ -1254,7 +1353,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                 }
+#ifdef LGS_NEAR_UNROLLED
                 near16(rows16, top);
+#else
+                near16r(rows16, top);
+#endif
             }
             if constexpr (OZ) {  // visible to the block at the next panel's staging barrier
                 if (__builtin_amdgcn_ballot_w64(pnz) != 0 && lane == 0) atomicOr(&nzm[pk >> 5], 1u << (pk & 31));
@@ -1350,9 +1453,13 @@ __global__ __launch_bounds__(256) void samplez_probe_kernel(const double* __rest
 // sel[c*n_keep + k] = proposal index of the state retained after step
 // (k+1)*thin (-1 = the carried-in state); cnt[p] / cnt_carry[c] count the
 // retained steps spent in each state (moments), final_sel[c] = last state.
+__device__ __forceinline__ bool aborted(const unsigned int* abort) {
+    return abort && (*(const volatile unsigned int*)abort & kAbortMask) != 0u;
+}
+
 __global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= a.nc) return;
+    if (c >= a.nc || aborted(a.abort)) return;
     double lw_x = a.lw_state[c];
     int64_t cur = -1;
     int64_t acc = 0;
@@ -1412,7 +1519,9 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
                                                             int64_t T, const int64_t* __restrict__ fsel,
                                                             int d, int64_t chunk,
                                                             unsigned long long* mom,
-                                                            OT* __restrict__ zs, int zs_cm, int64_t nc) {
+                                                            OT* __restrict__ zs, int zs_cm, int64_t nc,
+                                                            const unsigned int* abort) {
+    if (aborted(abort)) return;
     const int i0 = blockIdx.y * RY;
     const int64_t p0 = (int64_t)blockIdx.x * chunk;
     const int64_t p1 = p0 + chunk < n ? p0 + chunk : n;
@@ -1514,7 +1623,9 @@ template <typename ZT>
 __global__ __launch_bounds__(256) void moments_carry_kernel(const ZT* __restrict__ zs,
                                                             int coord_major, int64_t nc, int d,
                                                             const int32_t* __restrict__ cc,
-                                                            unsigned long long* mom) {
+                                                            unsigned long long* mom,
+                                                            const unsigned int* abort) {
+    if (aborted(abort)) return;
     const int i = blockIdx.x;
     long long s1 = 0, s2 = 0;
     for (int64_t c = threadIdx.x; c < nc; c += blockDim.x) {
@@ -1550,10 +1661,11 @@ __global__ __launch_bounds__(256) void gather_z_kernel(const ZT* __restrict__ Z,
                                                        int64_t nq, int64_t q_per_chain,
                                                        const OT* __restrict__ zs,
                                                        int zs_coord_major, int64_t nc, int d,
-                                                       OT* __restrict__ out, int out_coord_major) {
+                                                       OT* __restrict__ out, int out_coord_major,
+                                                       const unsigned int* abort) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int i = blockIdx.y;
-    if (q >= nq) return;
+    if (q >= nq || aborted(abort)) return;
     const int64_t s = sel[q];
     OT v;
     if (s >= 0) {
@@ -1585,12 +1697,46 @@ __global__ __launch_bounds__(256) void range16_kernel(const OT* __restrict__ zs,
 template <typename OT, typename ZT>
 __global__ __launch_bounds__(256) void carry_cols_kernel(const OT* __restrict__ zs, int zs_coord_major,
                                                          int64_t nc, int d, ZT* __restrict__ Z,
-                                                         int64_t ldz, int64_t col0) {
+                                                         int64_t ldz, int64_t col0, unsigned int* flags) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int i = blockIdx.y;
     if (c >= nc) return;
     const OT v = zs_coord_major ? zs[(size_t)i * nc + c] : zs[(size_t)c * d + i];
+    if (sizeof(ZT) == 2 && flags && (v > (OT)32767 || v < (OT)-32768)) atomicOr(flags, kFlagCarry16);
     Z[(size_t)i * ldz + col0 + c] = (ZT)v;
+}
+
+// Initial IMHK draws without a host round trip (lgs_imhk): *any = some chain has
+// init == 0; then each such chain takes its proposal (column c of Z) and weight.
+__global__ __launch_bounds__(256) void uninit_scan_kernel(const int32_t* __restrict__ init, int64_t nc,
+                                                          unsigned int* any) {
+    bool u = false;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x)
+        u |= init[c] == 0;
+    if (__builtin_amdgcn_ballot_w64(u) != 0 && (threadIdx.x & 63) == 0) atomicOr(any, 1u);
+}
+
+template <typename ZT, typename OT>
+__global__ __launch_bounds__(256) void init_apply_kernel(const ZT* __restrict__ Z, int32_t* __restrict__ init,
+                                                         int64_t nc, int d, const double* __restrict__ LW,
+                                                         OT* __restrict__ zs, int zs_cm, double* __restrict__ lws,
+                                                         unsigned int* flags) {
+    const bool ab = aborted(flags);
+    // the verification count so far (the initial draws'), kept if the block's own
+    // Klein launch is discarded
+    if (blockIdx.x == 0 && threadIdx.x == 0) flags[kFlagWordCheckpoint] = ab ? 0u : flags[kFlagWordResolved];
+    if (flags[kFlagWordUninit] == 0u || ab) return;
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nc || init[c] != 0) return;
+    for (int i = 0; i < d; ++i) {
+        const OT v = (OT)Z[(size_t)i * nc + c];
+        if (zs_cm)
+            zs[(size_t)i * nc + c] = v;
+        else
+            zs[(size_t)c * d + i] = v;
+    }
+    lws[c] = LW[c];
+    init[c] = 1;
 }
 
 // Z[coord][p] (ld ldz) -> out[p][coord] (row-major n x d), 64x64 tiles via LDS.
@@ -1649,7 +1795,8 @@ __global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, 
                                                       const double* __restrict__ BT, int d,
                                                       int64_t n, double* __restrict__ V,
                                                       int64_t ldv, int64_t rb, int64_t rstride,
-                                                      int64_t roff) {
+                                                      int64_t roff, const unsigned int* abort) {
+    if (aborted(abort)) return;  // (whole grid) the selections were not written
     constexpr int BM = 64, BN = 64, KC = 16, LDP = 80;  // LDP: padded row (doubles)
     __shared__ double As[KC][LDP];
     __shared__ double Bs[KC][LDP];
@@ -1743,7 +1890,8 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
                                                     int64_t rb, int64_t rstride, int64_t roff,
                                                     unsigned int* flags, int tx_count, int64_t ty_count,
                                                     const int16_t* __restrict__ h16, int64_t h16_lanes,
-                                                    int64_t hcols) {
+                                                    int64_t hcols, const unsigned int* abort) {
+    if (aborted(abort)) return;  // (whole grid) the selections were not written
     constexpr int TA = LGS_BZ_TA;  // 32-sample MFMA tiles per wave
     constexpr int BM = 64 * TA, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
     constexpr int KPT = KC * BM / 256;  // coefficients per thread per chunk
@@ -2023,7 +2171,7 @@ hipError_t accept(const AcceptArgs& a, hipStream_t st) {
 
 hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int64_t T,
                          const int64_t* fsel, int d, unsigned long long* mom, void* zs, int ob,
-                         int zs_cm, int64_t nc, hipStream_t st) {
+                         int zs_cm, int64_t nc, hipStream_t st, const unsigned int* abort) {
     if (n <= 0) return hipSuccess;
     const int64_t chunk = 16384;  // multiple of 4
     constexpr int RY = 4;  // rows per workgroup, vector path
@@ -2034,26 +2182,42 @@ hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt,
                      (!cnt || ((uintptr_t)cnt % 16) == 0);
     LGS_ZT(zb, ZT, LGS_ZT(ob, OT, {
         if (vec)
-            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, true, RY>), gridv, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc);
+            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, true, RY>), gridv, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort);
         else
-            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, false>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc);
+            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, false>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort);
     }));
     return hipGetLastError();
 }
 
 hipError_t moments_carry(const void* zs, int zb, int coord_major, int64_t nc, int d,
-                         const int32_t* cc, unsigned long long* mom, hipStream_t st) {
+                         const int32_t* cc, unsigned long long* mom, hipStream_t st,
+                         const unsigned int* abort) {
     if (nc <= 0) return hipSuccess;
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(moments_carry_kernel<ZT>, dim3(d), dim3(256), 0, st, (const ZT*)zs, coord_major, nc, d, cc, mom));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(moments_carry_kernel<ZT>, dim3(d), dim3(256), 0, st, (const ZT*)zs, coord_major, nc, d, cc, mom, abort));
     return hipGetLastError();
 }
 
 hipError_t gather_z(const void* Z, int zb, int64_t ldz, const int64_t* sel, int64_t nq,
                     int64_t q_per_chain, const void* zs, int ob, int zs_coord_major, int64_t nc,
-                    int d, void* out, int out_coord_major, hipStream_t st) {
+                    int d, void* out, int out_coord_major, hipStream_t st, const unsigned int* abort) {
     if (nq <= 0) return hipSuccess;
     const dim3 grid((unsigned)((nq + 255) / 256), (unsigned)d);
-    LGS_ZT(zb, ZT, LGS_ZT(ob, OT, hipLaunchKernelGGL((gather_z_kernel<ZT, OT>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, nq, q_per_chain, (const OT*)zs, zs_coord_major, nc, d, (OT*)out, out_coord_major)));
+    LGS_ZT(zb, ZT, LGS_ZT(ob, OT, hipLaunchKernelGGL((gather_z_kernel<ZT, OT>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, nq, q_per_chain, (const OT*)zs, zs_coord_major, nc, d, (OT*)out, out_coord_major, abort)));
+    return hipGetLastError();
+}
+
+hipError_t uninit_scan(const int32_t* init, int64_t nc, unsigned int* any, hipStream_t st) {
+    if (nc <= 0) return hipSuccess;
+    const unsigned g = (unsigned)std::min<int64_t>((nc + 255) / 256, 1024);
+    hipLaunchKernelGGL(uninit_scan_kernel, dim3(g), dim3(256), 0, st, init, nc, any);
+    return hipGetLastError();
+}
+
+hipError_t init_apply(const void* Z, int zb, int32_t* init, int64_t nc, int d, const double* LW, void* zs,
+                      int ob, int zs_cm, double* lws, unsigned int* flags, hipStream_t st) {
+    if (nc <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((nc + 255) / 256));
+    LGS_ZT(zb, ZT, LGS_ZT(ob, OT, hipLaunchKernelGGL((init_apply_kernel<ZT, OT>), grid, dim3(256), 0, st, (const ZT*)Z, init, nc, d, LW, (OT*)zs, zs_cm, lws, flags)));
     return hipGetLastError();
 }
 
@@ -2065,10 +2229,10 @@ hipError_t check_range16(const void* zs, int ob, int64_t count, unsigned int* fl
 }
 
 hipError_t carry_cols(const void* zs, int ob, int zs_coord_major, int64_t nc, int d, void* Z, int zb,
-                      int64_t ldz, int64_t col0, hipStream_t st) {
+                      int64_t ldz, int64_t col0, hipStream_t st, unsigned int* flags) {
     if (nc <= 0) return hipSuccess;
     const dim3 grid((unsigned)((nc + 255) / 256), (unsigned)d);
-    LGS_ZT(ob, OT, LGS_ZT(zb, ZT, hipLaunchKernelGGL((carry_cols_kernel<OT, ZT>), grid, dim3(256), 0, st, (const OT*)zs, zs_coord_major, nc, d, (ZT*)Z, ldz, col0)));
+    LGS_ZT(ob, OT, LGS_ZT(zb, ZT, hipLaunchKernelGGL((carry_cols_kernel<OT, ZT>), grid, dim3(256), 0, st, (const OT*)zs, zs_coord_major, nc, d, (ZT*)Z, ldz, col0, flags)));
     return hipGetLastError();
 }
 
@@ -2090,10 +2254,10 @@ hipError_t to_coord_major(const void* in, int ib, int64_t n, int d, void* Z, int
 
 hipError_t bz(const void* Z, int zb, int64_t ldz, const int64_t* sel, const double* BT, int d,
               int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
-              hipStream_t st) {
+              hipStream_t st, const unsigned int* abort) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_gemm_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, BT, d, n, V, ldv, rb, rstride, roff));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_gemm_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, BT, d, n, V, ldv, rb, rstride, roff, abort));
     return hipGetLastError();
 }
 
@@ -2102,7 +2266,7 @@ hipError_t gemm_f64(const double* X, int64_t ldx, const double* MT, int d, int64
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
     hipLaunchKernelGGL(bz_gemm_kernel<double>, grid, dim3(256), 0, st, X, ldx, nullptr, MT, d, n, V,
-                       (int64_t)d, n, (int64_t)0, (int64_t)0);
+                       (int64_t)d, n, (int64_t)0, (int64_t)0, (const unsigned int*)nullptr);
     return hipGetLastError();
 }
 
@@ -2130,13 +2294,13 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
-                 hipStream_t st) {
+                 hipStream_t st, const unsigned int* abort) {
     if (n <= 0) return hipSuccess;
     if (d % 16 != 0 || LGS_BZ_TA != 1) h16 = nullptr;  // history blocks must align with the chunks
     const int tx = ((d + 127) / 128 + LGS_BZ_TXPER - 1) / LGS_BZ_TXPER;  // coordinate-tile groups
     const int64_t ty = (n + 64 * LGS_BZ_TA - 1) / (64 * LGS_BZ_TA);
     const dim3 grid((unsigned)(tx * ((ty + 7) / 8) * 8));  // whole rounds of 8 XCDs (extra tiles exit)
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort));
     return hipGetLastError();
 }
 

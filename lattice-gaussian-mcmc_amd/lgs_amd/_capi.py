@@ -36,7 +36,7 @@ LGS_X_I32 = 0x100
 LGS_X_I64 = 0x200
 
 KERNEL_KLEIN, KERNEL_BZ, KERNEL_ACCEPT, KERNEL_MOMENTS = 0, 1, 2, 3
-KERNEL_GRAM, KERNEL_SERIES = 4, 5
+KERNEL_GRAM, KERNEL_SERIES, KERNEL_KLEIN_INIT = 4, 5, 6
 LGS_COUNTER_RESOLVED = 0
 LGS_COUNTER_FALLBACK = 1
 
