@@ -78,3 +78,45 @@ def test_wang_ling_imhk_subset_bit_exact(oracle, cfg, _, m):
     np.testing.assert_allclose(lw.cpu().numpy()[:m], lwo, rtol=1e-9, atol=1e-9)
     rate = acc.sum().item() / (nc * T)
     assert 0.0 < rate <= 1.0
+
+
+ACC_CASES = [("C3_ntru512", 1 << 14, 1024), ("C4_qary1024", 1 << 14, 1024), ("C5_ntru2048", 1 << 11, 256)]
+
+
+@pytest.mark.parametrize("cfg,nc,m", ACC_CASES)
+def test_imhk_acceptance_vs_cpu(oracle, cfg, nc, m):
+    """IMHK acceptance against the CPU reference (imhk.py:141-177), north_star
+    'acceptance within +-1 % of CPU reference', at C3, C4 and C5:
+    * reference-mode weights: every proposal accepted on the GPU (1.0 exactly),
+      as in the reference (its weight is a constant up to rounding);
+    * Wang-Ling weights: the oracle runs the first m chains x 4 steps on the same
+      counters -- every accept decision and final state is bit-equal -- and the
+      GPU's acceptance over all nc chains is within 1 % (absolute) of the oracle's
+      (or 4 standard errors of the oracle estimate, whichever is larger)."""
+    import torch
+    from lgs_amd import _capi
+    B, R, cp, sigma = _setup(cfg, oracle)
+    d = B.shape[0]
+    ctx = _capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    T, seed = 4, 2027
+    res = {}
+    for wl in (False, True):
+        z = torch.zeros((d, nc), dtype=torch.int32, device="cuda")
+        lw = torch.zeros(nc, dtype=torch.float64, device="cuda")
+        init = torch.zeros(nc, dtype=torch.int32, device="cuda")
+        acc = torch.zeros(nc, dtype=torch.int64, device="cuda")
+        f = _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR | (_capi.LGS_WANG_LING if wl else 0)
+        ctx.imhk(seed, 0, nc, 1, T, 1, z, lw, init, acc, flags=f)
+        res[wl] = (acc.cpu().numpy(), z[:, :m].cpu().numpy().T)
+    assert res[False][0].sum() == nc * T  # reference mode: acceptance 1.0
+    acc_wl, z_wl = res[True]
+    zo, _, acco = oracle.imhk_parallel(R, cp, B, sigma, m, T, seed=seed, first_step=1,
+                                       mode=oracle.IMHK_WANG_LING, threads=16)
+    assert np.array_equal(acc_wl[:m], acco)  # bit-equal decisions on the CPU subset
+    assert np.array_equal(z_wl, zo)
+    gpu, cpu = acc_wl.sum() / (nc * T), acco.sum() / (m * T)
+    se = np.sqrt(max(cpu * (1 - cpu), 1e-4) / (m * T))
+    assert abs(gpu - cpu) < max(0.01, 4 * se), (gpu, cpu, se)
+    print(f"{cfg}: Wang-Ling acceptance GPU {gpu:.4f} ({nc} chains) vs CPU oracle {cpu:.4f} ({m} chains), "
+          f"se {se:.4f}; reference mode 1.0")
