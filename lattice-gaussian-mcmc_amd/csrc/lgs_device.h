@@ -1070,11 +1070,9 @@ __device__ __forceinline__ double sample_z_coord(double mu, double u, QP q, int 
                                     log_norm, dmu);
     return z;
 }
-// The same with the certificate fixed at compile time (hot loops: one call target).
-// The same with the certificate fixed at compile time (hot loops: one call target);
-// CERT: always returns a decision (a guess when not covered: amb = true, log_norm = 0).
 // The capped kind with sigma >= 360 alone (klein_mfma_kernel dispatches on the
-// kind itself): a small leaf, no kind dispatch inside.
+// kind itself): a small leaf, no kind dispatch inside (inlined into the rolled
+// near field, LGS_CAPPED_INLINE).
 template <bool CERT, typename QP>
 #ifdef LGS_CAPPED_INLINE
 __device__ __forceinline__
@@ -1111,13 +1109,6 @@ __device__ __forceinline__ double sz_finish(SzPair r, double mu, double u, QP q,
     }
     if (amb) log_norm = 0.0;
     return z;
-}
-template <bool CERT, typename TP, typename QP>
-__device__ __forceinline__ double sample_z_coord_t(double mu, double u, QP q, int precision,
-                                                   bool linear_probs, bool want_log, TP etab,
-                                                   double& log_norm, double dmu, bool& amb) {
-    const SzPair r = sample_z_coord_leaf<CERT>(mu, u, q, precision, linear_probs, want_log, etab, dmu);
-    return sz_finish<CERT>(r, mu, u, q, precision, linear_probs, want_log, etab, log_norm, dmu, amb);
 }
 
 // Conditional mean of coordinate i in the reference's order (klein.py:191-195:

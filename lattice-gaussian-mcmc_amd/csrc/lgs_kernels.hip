@@ -273,40 +273,6 @@ __device__ __forceinline__ double resolve_coord(const KleinArgs& a, int i, const
     return r.z;
 }
 
-// mu_exact_col from the int16 history of the int8-digit far field (z + 128, exact
-// for |z| <= 32639, which the OZ kernel guarantees): the 16 coefficients of a
-// 16-coordinate block are 32 contiguous bytes of the lane, so the column costs d/16
-// loads instead of d strided ones (whose latency would dominate a replay).
-__device__ __noinline__ double mu_exact_hist(const double* __restrict__ R, const int16_t* __restrict__ hl,
-                                             int64_t lanes, int shift, int i, int d, double cp, double rii) {
-    const double* __restrict__ Ri = R + (size_t)i * d;
-    const size_t bstride = (size_t)lanes * 16;  // int16 elements between 16-coordinate blocks
-    double cs = 0.0;
-    const int b0 = (i + 1 + shift) >> 4, bl = (d - 1 + shift) >> 4;
-    v4u_t w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0};
-    if (b0 <= bl) {
-        w0 = ((const v4u_t*)(hl + (size_t)b0 * bstride))[0];
-        w1 = ((const v4u_t*)(hl + (size_t)b0 * bstride))[1];
-    }
-    for (int b = b0; b <= bl; ++b) {
-        v4u_t n0 = w0, n1 = w1;
-        if (b < bl) {  // next block in flight while this one is summed
-            n0 = ((const v4u_t*)(hl + (size_t)(b + 1) * bstride))[0];
-            n1 = ((const v4u_t*)(hl + (size_t)(b + 1) * bstride))[1];
-        }
-        const int j0 = b * 16 - shift;  // coordinate at position 0 of the block
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const unsigned int wd = k < 8 ? w0[(k >> 1) & 3] : w1[(k >> 1) & 3];
-            const int h = (int)(int16_t)(uint16_t)((k & 1) ? (wd >> 16) : (wd & 0xffffu));  // signed
-            const int j = j0 + k;
-            if (j > i && j < d) cs = cs + Ri[j] * (double)(h - 128);
-        }
-        w0 = n0;
-        w1 = n1;
-    }
-    return (cp - cs) / rii;
-}
 
 // Reference-order conditional mean of coordinate i of ONE sample (lane L of the
 // calling wave), computed by the whole wave: lane k loads R_ij and z_j of

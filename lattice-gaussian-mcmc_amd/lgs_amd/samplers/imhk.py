@@ -151,7 +151,12 @@ class IMHKSampler(DiscreteGaussianSampler):
             break
         z = zs[0].astype(np.int64)
         self._sbuf = {"z": z, "lw": lws[0].copy(), "acc": accd[0].astype(bool),
-                      "v": ctx.lattice_points(z), "first": self._next_step, "flags": flags, "pos": 0}
+                      "v": ctx.lattice_points(z), "first": self._next_step, "pos": 0, "key": self._block_key()}
+
+    def _block_key(self):
+        """What a look-ahead block was drawn with: the counters (seed, chain id), the
+        call flags and the context (basis) -- a block is served only while all match."""
+        return (self.seed, self.chain_id, self._flags(), id(self.context))
 
     def step(self) -> Tuple[np.ndarray, bool]:
         """One MCMC step (imhk.py:141-177): (new_state, accepted).  Served from a
@@ -159,7 +164,7 @@ class IMHKSampler(DiscreteGaussianSampler):
         caller keeps stepping), identical to launching every step on its own."""
         b = self._sbuf
         if (b is None or b["pos"] >= len(b["lw"]) or b["first"] + b["pos"] != self._next_step
-                or b["flags"] != self._flags()):
+                or b["key"] != self._block_key()):
             if b is not None and b["pos"] >= len(b["lw"]):
                 self._step_block = min(2 * self._step_block, 1024)
             self._fill_steps(self._step_block)

@@ -49,6 +49,12 @@ def test_buffered_step_equals_single_launches(wang_ling):
     assert a.accepted_proposals == b.accepted_proposals
     if wang_ling:
         assert not all(acc_a), "expected rejections with the Wang-Ling weight"
+    # changing the counters between steps drops the look-ahead block:
+    # the next steps use the new seed / chain id, as an unbuffered launch does
+    a.seed = b.seed = 777
+    both(4)
+    a.chain_id = b.chain_id = 11
+    both(4)
 
 
 def test_imhk_trace_matches_oracle(oracle):
