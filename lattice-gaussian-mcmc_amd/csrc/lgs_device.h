@@ -815,12 +815,35 @@ __device__ __forceinline__ cdptr cap_coef() {
     asm volatile("" : "+s"(p));
     return p;
 }
+// Coefficients in SGPRs: Estrin's first level (both operands constants) costs a
+// VGPR copy per pair; a two-way Horner split (even and odd coefficients as two
+// interleaved Horner chains in x^2, each FMA with its scalar coefficient as the
+// addend) needs no copies at about half Horner's depth.  LGS_CAP_ESTRIN: Estrin.
 template <int N>
 __device__ __forceinline__ double poly_estrin_p(cdptr cf, double x) {
     double c[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) c[k] = cf[k];
+#ifdef LGS_CAP_ESTRIN
     return poly_estrin(c, x);
+#else
+    // v_fma_f64 with the scalar coefficient as the addend, written out: left to
+    // itself the compiler picks v_fmac_f64 and copies the coefficient into the
+    // accumulator register first
+    auto fma_s = [](double a, double b, double sc) {
+        double r;
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(sc));
+        return r;
+    };
+    const double x2 = x * x;
+    constexpr int NE = (N + 1) / 2, NO = N / 2;  // c[0], c[2], ... and c[1], c[3], ...
+    double pe = c[2 * (NE - 1)], po = c[2 * (NO - 1) + 1];
+#pragma unroll
+    for (int k = NE - 2; k >= 0; --k) pe = fma_s(pe, x2, c[2 * k]);
+#pragma unroll
+    for (int k = NO - 2; k >= 0; --k) po = fma_s(po, x2, c[2 * k + 1]);
+    return fma(po, x, pe);
+#endif
 }
 
 // C(k) - base of a capped window with sigma >= 360 (Euler-Maclaurin with 3 terms,

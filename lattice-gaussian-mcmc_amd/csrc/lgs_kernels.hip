@@ -1214,7 +1214,10 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                 for (int j = 0; j < 8; ++j) hp[j] = 0u;
                 int flm = 0;
                 typedef double d2v __attribute__((ext_vector_type(2)));
-#pragma nounroll
+#ifndef LGS_NEAR_UNROLL  // coordinates per loop iteration (the running sums shift by one per step)
+#define LGS_NEAR_UNROLL 1
+#endif
+#pragma unroll LGS_NEAR_UNROLL
                 for (int s = 0; s < rows16; ++s) {
                     const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
                     const lds_cdptr rec = (lds_cdptr)rec_lds + (i - (p_hi - 32)) * kRecStride;
@@ -1236,17 +1239,20 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         LGS_DC_ADD(8 + kind, 1);
                     }
 #endif
+                    // stores: v_cvt_i32_f64 saturates, so no clamps -- a value beyond the
+                    // int16 history's range (or a 16-bit store's) flags kFlagOverflow16 and
+                    // the launch is redone wider; beyond int32 is an error (kFlagOverflow)
                     if constexpr (sizeof(ZT) == 8) {
                         Z[(size_t)i * ldz + p] = (ZT)(int64_t)zi;
                     } else {
                         if (sizeof(ZT) == 4 && !(zi <= 2147483647.0 && zi >= -2147483648.0)) flags |= kFlagOverflow;
-                        if (sizeof(ZT) == 2 && !(zi <= 32767.0 && zi >= -32768.0)) flags |= kFlagOverflow16;
-                        Z[(size_t)i * ldz + p] = (ZT)(int)fmin(fmax(zi, -2147483648.0), 2147483647.0);
+                        if (!OZ && sizeof(ZT) == 2 && !(zi <= 32767.0 && zi >= -32768.0)) flags |= kFlagOverflow16;
+                        Z[(size_t)i * ldz + p] = (ZT)(int)zi;
                     }
                     if constexpr (OZ) {
                         if (!(zi <= 32639.0 && zi >= -32767.0)) flags |= kFlagOverflow16;
-                        // int16 history value (z + 128, clamped to the far field's digit range)
-                        const unsigned int hv = (unsigned int)((int)(fmin(fmax(zi, -32767.0), 32639.0) + 128.0)) & 0xffffu;
+                        // int16 history value z + 128 (exact whenever the range check passed)
+                        const unsigned int hv = (unsigned int)((int)zi + 128) & 0xffffu;
                         if (hblock) {
 #pragma unroll
                             for (int j = 7; j >= 1; --j) hp[j] = __builtin_amdgcn_alignbit(hp[j], hp[j - 1], 16);
