@@ -1,7 +1,11 @@
 """Per-launch Klein-kernel counters of a rocprofv3 profile of bench.py -> JSON for
 bench.py's roofline (tools/gpu_roofline.sh).
 
-usage: roofline_counters.py <profile dir> <config> <units_per_launch> <d> <out.json>
+usage: roofline_counters.py <profile dir> <config> <units_per_launch> <d> <out.json> [bench_trace.log]
+
+The build id of the library the profiled bench loaded (its JSON line's
+roofline.build_id, from the optional log) is stored with the counters: bench.py
+uses a counters file only for that same build.
 
 Every counter_collection.csv under the profile dir is read; rows of the Klein
 kernel's largest dispatches (the bench's 2^20-proposal launches) are averaged per
@@ -19,6 +23,11 @@ import sys
 from collections import defaultdict
 
 root, config, units, d, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+build_id = None
+if len(sys.argv) > 6 and os.path.exists(sys.argv[6]):
+    lines = [x for x in open(sys.argv[6]) if x.startswith("{")]
+    if lines:
+        build_id = json.loads(lines[-1]).get("roofline", {}).get("build_id")
 vals = defaultdict(list)
 grid_max = 0
 rows_all = []
@@ -37,7 +46,7 @@ avg = {k: sum(v) / len(v) for k, v in vals.items()}
 waves = avg.get("SQ_WAVES")
 n_panels = (d + 31) // 32
 f64_mfma = (waves or 0) * 16 * max(n_panels - 1, 0)
-res = {"config": config, "units_per_launch": units, "grid_size": grid_max,
+res = {"config": config, "units_per_launch": units, "grid_size": grid_max, "build_id": build_id,
        "counters_per_launch": avg,
        "fp64_flops": 64 * (2 * avg.get("SQ_INSTS_VALU_FMA_F64", 0) + avg.get("SQ_INSTS_VALU_MUL_F64", 0)
                            + avg.get("SQ_INSTS_VALU_ADD_F64", 0)) + 2048 * f64_mfma,
