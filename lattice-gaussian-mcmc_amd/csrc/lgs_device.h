@@ -870,24 +870,20 @@ __device__ __forceinline__ double capped_C(double kd, double m, double sig, doub
 // the series erf / exp (PolyErf), and the +-1 walk only behind a wave-uniform test
 // (the guess is off by one for ~4e-5 of the lanes).  Same decision rule, margins
 // and certificate as sample_z_wide.
-template <bool CERT, typename QP>
-__device__ __forceinline__ double sample_z_capped(double mu, double u, const QHead& h, QP q, bool want_log,
-                                                  double& log_norm, double dmu) {
-    const double sig = h.v[0], is = h.v[1];
-    const double c = rint(mu);
-    const double m = mu - c;
-    double cS[kSzDeg + 1], cB[kSzDeg + 1];
-#pragma unroll
-    for (int k = 0; k <= kSzDeg; ++k) {
-        cS[k] = q[kSzS + k];
-        cB[k] = q[kSzB + k];
-    }
-    const double S = poly_estrin(cS, m), base = poly_estrin(cB, m);
-    const double target = u * S;
-    // continuous quantile x = m + sigma sqrt(2) erfinv(v): erfinv(v) = v R(v^2)
+// The capped decision by evaluating C(k) at the guess (+-1 walk behind a
+// wave-uniform test): the waves where some lane's quantile decision is not
+// certain (sample_z_capped).  Out of line: its registers stay out of the Klein
+// kernels' rolled near field, which runs it for ~0.1 % of the waves.
+// (Both results come back in registers: a reference parameter of a call lives in
+// the caller's scratch frame, a store per call that the next call waits for.)
+struct SzPair {
+    double z, ln;
+};
+template <bool CERT>
+__device__ __noinline__ SzPair capped_slow(double c, double m, double sig, double is, double S, double base,
+                                           double target, double xg, bool want_log, double dmu) {
     const cdptr cf = cap_coef();
-    const double v = fmin(fmax((target + base) * h.v[4], -0.8485), 0.8485);
-    const double xg = fma(h.v[5] * v, poly_estrin_p<13>(cf + kCapRI, v * v), m);
+    SzPair r = {__builtin_nan(""), 0.0};
     double kd = fmin(fmax(ceil(xg - 0.5), -500.0), 500.0);
     double fk;
     double Ck = capped_C(kd, m, sig, is, base, fk, cf);
@@ -907,16 +903,93 @@ __device__ __forceinline__ double sample_z_capped(double mu, double u, const QHe
     }
     const double margin = fmin(Ck - target, kd > -500.0 ? target - (Ck - fk) : target);
     if constexpr (CERT) {
-        if (!(Ck > target)) return __builtin_nan("");
+        if (!(Ck > target)) return r;
         if (!(margin > fma(0.6 * dmu, is, 1e-12) * S) || !(fabs(m) + 1.01 * dmu < 0.5)) {
-            log_norm = __builtin_nan("");
-            return c + kd;
+            r.z = c + kd;
+            r.ln = __builtin_nan("");
+            return r;
         }
     } else if (!(margin > 1e-12 * S) || !(Ck > target)) {
-        return __builtin_nan("");
+        return r;
     }
-    log_norm = want_log ? log(S) : 0.0;
-    return c + kd;
+    r.z = c + kd;
+    r.ln = want_log ? log(S) : 0.0;
+    return r;
+}
+
+#ifdef LGS_DIAG_CAPQ
+__device__ unsigned long long lgs_diag_capq[8];
+#endif
+template <bool CERT, typename QP>
+__device__ __forceinline__ double sample_z_capped(double mu, double u, const QHead& h, QP q, bool want_log,
+                                                  double& log_norm, double dmu) {
+    const double sig = h.v[0], is = h.v[1];
+    const double c = rint(mu);
+    const double m = mu - c;
+    double cS[kSzDeg + 1], cB[kSzDeg + 1];
+#pragma unroll
+    for (int k = 0; k <= kSzDeg; ++k) {
+        cS[k] = q[kSzS + k];
+        cB[k] = q[kSzB + k];
+    }
+    const double S = poly_estrin(cS, m), base = poly_estrin(cB, m);
+    const double target = u * S;
+    // continuous quantile x = m + sigma sqrt(2) erfinv(v): erfinv(v) = v R(v^2)
+    const cdptr cf = cap_coef();
+    const double v = fmin(fmax((target + base) * h.v[4], -0.8485), 0.8485);
+    const double xg = fma(h.v[5] * v, poly_estrin_p<13>(cf + kCapRI, v * v), m);
+#ifdef LGS_DIAG_CAP_GUESS  // diagnostic builds only (NOT bit-exact): cost probe, decision = the guess
+    return c + fmin(fmax(ceil(xg - 0.5), -500.0), 500.0);
+#endif
+#ifndef LGS_CAP_NO_QUANTILE
+    // Decision from the quantile alone, without evaluating C(k): with the window
+    // sums C(k) of this kind (sigma >= 360), C(k) + base = sc erf(t(y_k) / sqrt 2)
+    // at y_k = k + 1/2 + (k - m) / (24 sigma^2) to within 4e-11 units of y
+    // (mpmath over sigma in [360, 1e10], every 7th k, tools/capped_quantile_check.py),
+    // so C(k) > u S  <=>  k > xs = xg - 1/2 - (xg - m) / (24 sigma^2), and the decision
+    // is floor(xs) + 1 whenever xs is farther from an integer than xs's error:
+    // the erfinv polynomial's 2.93e-8 relative (|xg - m| <= 501.5), the reference's
+    // fp64 cumsum within 1e-12 S (2.7e-9 units: f >= 0.379 over the window), fp64
+    // rounding (< 1e-11 units), and for certified decisions a mean shift of up to
+    // dmu (the boundary moves <= 0.6 dmu S / (sigma f) <= 4.5 dmu units, the
+    // margin rule below in x units).  The rest (~3e-5 of the draws) go on below.
+    {
+        const double xs = fma((xg - m) * (-1.0 / 24.0), is * is, xg - 0.5);
+        const double fl = floor(xs);
+        const double tol = fma(2.94e-8, fabs(xg - m), CERT ? fma(4.5, dmu, 1e-8) : 1e-8);  // (plain: dmu < 0)
+#ifdef LGS_DIAG_CAPQ  // diagnostic builds only: why the quantile decision falls through
+        {
+            const bool ca = !(xs - fl > tol && fl + 1.0 - xs > tol), cb = !(fl >= -501.0 && fl <= 499.0),
+                       cc = !(fabs(v) < 0.848), cd = CERT && !(fabs(m) + 1.01 * dmu < 0.5);
+            const unsigned long long b0 = __builtin_amdgcn_ballot_w64(true), b1 = __builtin_amdgcn_ballot_w64(ca),
+                                     b2 = __builtin_amdgcn_ballot_w64(cb), b3 = __builtin_amdgcn_ballot_w64(cc),
+                                     b4 = __builtin_amdgcn_ballot_w64(cd),
+                                     b5 = __builtin_amdgcn_ballot_w64(ca || cb || cc || cd);
+            if ((threadIdx.x & 63) == __builtin_ctzll(b0)) {
+                atomicAdd(&lgs_diag_capq[0], (unsigned long long)__builtin_popcountll(b0));
+                atomicAdd(&lgs_diag_capq[1], (unsigned long long)__builtin_popcountll(b1));
+                atomicAdd(&lgs_diag_capq[2], (unsigned long long)__builtin_popcountll(b2));
+                atomicAdd(&lgs_diag_capq[3], (unsigned long long)__builtin_popcountll(b3));
+                atomicAdd(&lgs_diag_capq[4], (unsigned long long)__builtin_popcountll(b4));
+                atomicAdd(&lgs_diag_capq[5], b5 != 0 ? 1ull : 0ull);
+                atomicAdd(&lgs_diag_capq[6], 1ull);
+            }
+            atomicMax(&lgs_diag_capq[7], (unsigned long long)(dmu * 1e15));
+        }
+#endif
+        const bool fast = xs - fl > tol && fl + 1.0 - xs > tol && fl >= -501.0 && fl <= 499.0 &&
+                          fabs(v) < 0.848 && (!CERT || fabs(m) + 1.01 * dmu < 0.5);
+        // a wave-uniform branch: the evaluation below must not be if-converted into
+        // straight-line code that every wave runs
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(!fast) == 0, 1)) {
+            log_norm = want_log ? log(S) : 0.0;
+            return c + (fl + 1.0);
+        }
+    }
+#endif
+    const SzPair r = capped_slow<CERT>(c, m, sig, is, S, base, target, xg, want_log, dmu);
+    log_norm = r.ln;
+    return r.z;
 }
 
 // Both window ends evaluated per draw (kinds without precomputed normalisers);
@@ -1049,11 +1122,6 @@ __device__ __forceinline__ double sample_z_coord_body(double mu, double u, QP qi
                : sample_z_wide<3, CERT>(mu, u, qh, q, kind, precision, linear_probs, want_log, etab, log_norm, dmu);
 }
 
-// Both results come back in registers (a reference parameter of a call lives in
-// the caller's scratch frame: a store per call that the next call waits for).
-struct SzPair {
-    double z, ln;
-};
 template <bool CERT, typename TP, typename QP>
 LGS_SAMPLEZ_ATTR SzPair sample_z_coord_leaf(double mu, double u, QP q, int precision,
                                             bool linear_probs, bool want_log, TP etab, double dmu) {

@@ -2290,3 +2290,13 @@ extern "C" __attribute__((visibility("default"))) int lgs_diag_cycles_read(unsig
     return hipMemcpyToSymbol(HIP_SYMBOL(lgs::lgs_diag_cycles), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif
+#ifdef LGS_DIAG_CAPQ
+// Diagnostic builds only: read and reset the capped-quantile counters (lgs_device.h).
+extern "C" __attribute__((visibility("default"))) int lgs_diag_capq_read(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lgs::lgs_diag_capq), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    unsigned long long zero[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lgs::lgs_diag_capq), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -452,6 +452,32 @@ def test_samplez_near_boundaries(ctx):
             np.testing.assert_allclose(ln, ln_t, rtol=1e-13, atol=1e-13)
 
 
+def test_samplez_capped_quantile_near_boundaries(ctx):
+    """The capped kind (sigma >= 360, window rint(mu) +- 500) decides most draws from
+    the quantile alone (lgs_device.h sample_z_capped): u placed just around exact
+    CDF boundaries (long-double sums) over sigma in [360, 1e10] and m over
+    [-1/2, 1/2], including the window's first and last points, equals the table walk."""
+    rng = np.random.default_rng(79)
+    mus, sigs, us = [], [], []
+    for _ in range(200):
+        sig = float(np.exp(rng.uniform(np.log(360.0), np.log(1e10))))
+        mu = float(rng.uniform(-0.5, 0.5) + rng.choice([0.0, 7.0, -1e6]))
+        c = np.rint(mu)
+        k = np.arange(c - 500, c + 501, dtype=np.longdouble)
+        w = np.exp(-0.5 * ((k - np.longdouble(mu)) / np.longdouble(sig)) ** 2)
+        F = np.cumsum(w) / np.sum(w)
+        for j in np.concatenate([[0, 1, 998, 999], rng.choice(len(F) - 1, 6)]):
+            for eps in (-1e-7, -1e-9, -3e-12, 3e-12, 1e-9, 1e-7):
+                u = float(F[j]) + eps
+                if 0.0 <= u < 1.0:
+                    mus.append(mu), sigs.append(sig), us.append(u)
+    mu, sig, u = np.array(mus), np.array(sigs), np.array(us)
+    z_t, ln_t = ctx.sample_z(mu, sig, u, table=True)
+    z, ln = ctx.sample_z(mu, sig, u)
+    assert np.array_equal(z, z_t)
+    np.testing.assert_allclose(ln, ln_t, rtol=1e-13, atol=1e-13)
+
+
 def test_samplez_tab_vs_libm_random(ctx):
     """Tabulated erf/exp path vs ocml libm path vs table walk on 400k random draws
     over sigma in [4, 1e6] (wide windows, capped and uncapped)."""

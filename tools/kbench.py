@@ -56,6 +56,12 @@ def run_one(args):
         out["decisions_per_wave"] = {names[3 + k]: round(dbuf[8 + k] / waves, 1) for k in range(5)}
         out["cycles_per_decision"] = {names[3 + k]: round(dbuf[3 + k] / max(dbuf[8 + k], 1), 1)
                                       for k in range(5)}
+    capq = getattr(_capi.load_library(), "lgs_diag_capq_read", None)
+    if capq is not None:
+        qb = (ctypes.c_ulonglong * 8)()
+        capq(qb)
+        out["capq"] = {"lanes": qb[0], "tol": qb[1], "range": qb[2], "v": qb[3], "rint": qb[4],
+                       "waves_with_fail": qb[5], "waves": qb[6], "max_dmu": qb[7] * 1e-15}
     print(json.dumps(out), flush=True)
 
 
