@@ -820,12 +820,22 @@ __device__ __forceinline__ cdptr cap_coef() {
 // interleaved Horner chains in x^2, each FMA with its scalar coefficient as the
 // addend) needs no copies at about half Horner's depth.  LGS_CAP_ESTRIN: Estrin.
 template <int N>
+__device__ __forceinline__ double poly_h2(const double* c, double x);
+template <int N>
 __device__ __forceinline__ double poly_estrin_p(cdptr cf, double x) {
     double c[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) c[k] = cf[k];
+    return poly_h2<N>(c, x);
+}
+// the coefficients already in (scalar) registers
+template <int N>
+__device__ __forceinline__ double poly_h2(const double* c, double x) {
 #ifdef LGS_CAP_ESTRIN
-    return poly_estrin(c, x);
+    double cc[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) cc[k] = c[k];
+    return poly_estrin(cc, x);
 #else
     // v_fma_f64 with the scalar coefficient as the addend, written out: left to
     // itself the compiler picks v_fmac_f64 and copies the coefficient into the
@@ -920,9 +930,24 @@ __device__ __noinline__ SzPair capped_slow(double c, double m, double sig, doubl
 #ifdef LGS_DIAG_CAPQ
 __device__ unsigned long long lgs_diag_capq[8];
 #endif
+// The erfinv coefficients kCapCoef[kCapRI..] loaded into scalar registers ahead of
+// the decision (load_cap_ri, at the top of a coordinate's step: the scalar-memory
+// round trip then overlaps the record reads instead of sitting on the chain).
+struct CapRI {
+    double c[13];
+};
+__device__ __forceinline__ CapRI load_cap_ri() {
+    const cdptr cf = cap_coef();
+    CapRI r;
+#pragma unroll
+    for (int k = 0; k < 13; ++k) r.c[k] = cf[kCapRI + k];
+#pragma unroll
+    for (int k = 0; k < 13; ++k) asm volatile("" : "+s"(r.c[k]));
+    return r;
+}
 template <bool CERT, typename QP>
 __device__ __forceinline__ double sample_z_capped(double mu, double u, const QHead& h, QP q, bool want_log,
-                                                  double& log_norm, double dmu) {
+                                                  double& log_norm, double dmu, const CapRI* ri = nullptr) {
     const double sig = h.v[0], is = h.v[1];
     const double c = rint(mu);
     const double m = mu - c;
@@ -937,7 +962,7 @@ __device__ __forceinline__ double sample_z_capped(double mu, double u, const QHe
     // continuous quantile x = m + sigma sqrt(2) erfinv(v): erfinv(v) = v R(v^2)
     const cdptr cf = cap_coef();
     const double v = fmin(fmax((target + base) * h.v[4], -0.8485), 0.8485);
-    const double xg = fma(h.v[5] * v, poly_estrin_p<13>(cf + kCapRI, v * v), m);
+    const double xg = fma(h.v[5] * v, ri ? poly_h2<13>(ri->c, v * v) : poly_estrin_p<13>(cf + kCapRI, v * v), m);
 #ifdef LGS_DIAG_CAP_GUESS  // diagnostic builds only (NOT bit-exact): cost probe, decision = the guess
     return c + fmin(fmax(ceil(xg - 0.5), -500.0), 500.0);
 #endif

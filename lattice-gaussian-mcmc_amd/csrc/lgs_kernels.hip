@@ -107,12 +107,56 @@ __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double
     return zi;
 }
 
-// decide_coord with the coordinate's record rec staged in LDS (klein_mfma_kernel, 32-row panels).
+// A coordinate's Klein record (kRecStride doubles, staged in LDS per 32-row panel)
+// read into registers as one batch of 16-byte LDS reads at the top of the
+// coordinate's step, before anything branches on it: one LDS round trip per
+// coordinate instead of one per use site (mean, kind, window, polynomials,
+// weight terms, near-field coefficients), each behind the previous branch.
+// The capped kind's erfinv coefficients come along as scalar loads (LGS_CAP_RI_PRE).
+#ifndef LGS_CAP_NO_RI_PRE
+#define LGS_CAP_RI_PRE 1
+#endif
+constexpr int kRecHot = kRecRs + 16;  // through the 15 near-field coefficients (44 doubles)
+struct RecRegs {
+    double v[kRecHot];
+#ifdef LGS_CAP_RI_PRE
+    CapRI ri;
+#endif
+    __device__ __forceinline__ double operator[](int k) const { return v[k]; }
+};
+__device__ __forceinline__ RecRegs load_rec(lds_cdptr rec) {
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    using lds_d2p = const __attribute__((address_space(3))) d2v*;
+    RecRegs r;
+#pragma unroll
+    for (int k = 0; k < kRecHot / 2; ++k) {
+        const d2v t = ((lds_d2p)rec)[k];
+        r.v[2 * k] = t[0];
+        r.v[2 * k + 1] = t[1];
+    }
+#ifdef LGS_CAP_RI_PRE
+    r.ri = load_cap_ri();
+#endif
+#ifndef LGS_REC_NOPIN
+    // pinned here: left alone, the compiler sinks each read into the branch that
+    // uses it (three round trips after the kind / window branches)
+#pragma unroll
+    for (int k = 0; k < kRecHot; ++k) asm volatile("" : "+v"(r.v[k]));
+#endif
+    return r;
+}
+struct RecView {  // q[k] of the SampleZ functions, served from the registers
+    const RecRegs& r;
+    __device__ __forceinline__ double operator[](int k) const { return r.v[k]; }
+};
+
+// decide_coord with the coordinate's record rec staged in LDS (klein_mfma_kernel,
+// 32-row panels); rr: the record's registers (load_rec), rec for the rare paths.
 // LIBM: the SampleZ path without per-coordinate constants (LGS_SAMPLEZ_LIBM); a
 // separate kernel instantiation, so the default kernel carries one call path.
 template <bool WL, bool CERT, bool LIBM, typename TP>
 __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, double mu,
-                                                   lds_cdptr rec, CoordStream& rs, double& lw,
+                                                   lds_cdptr rec, const RecRegs& rr, CoordStream& rs, double& lw,
                                                    unsigned int& flags, TP etab, double dmu, bool& amb) {
     double zi = 0.0;
     amb = false;
@@ -120,7 +164,9 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         flags |= kFlagNonFinite;
         return 0.0;
     }
-    const QHead qh = load_head(rec);  // the fields branched on below, in one LDS round trip
+    QHead qh;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) qh.v[k] = rr[k];
     const double s = qh.v[0];
 #ifdef LGS_DIAG_NO_SAMPLEZ
     if (true) {
@@ -187,9 +233,14 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
 #endif
             {
 #ifndef LGS_NO_CAPPED_POLY
-            if (kind == kSzCapped && q7 == 1)  // sigma >= 360: the streamlined capped leaf
-                r = sample_z_capped_leaf<CERT>(mu, u, rec, WL, dmu);
-            else
+            if (kind == kSzCapped && q7 == 1) {  // sigma >= 360: the streamlined capped decision
+                r.ln = 0.0;
+#ifdef LGS_CAP_RI_PRE
+                r.z = sample_z_capped<CERT>(mu, u, qh, RecView{rr}, WL, r.ln, dmu, &rr.ri);
+#else
+                r.z = sample_z_capped<CERT>(mu, u, qh, RecView{rr}, WL, r.ln, dmu);
+#endif
+            } else
 #endif
                 r = sample_z_coord_leaf<CERT>(mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, dmu);
             zi = sz_finish<CERT>(r, mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, ln, dmu, amb);
@@ -198,7 +249,7 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         if (WL) lw += ln;
     }
     if (!WL) {
-        const double t = ref_weight(zi, mu, rec[kRecRos], rec[kRecIsr], rec[kRecLterm]);
+        const double t = ref_weight(zi, mu, rr[kRecRos], rr[kRecIsr], rr[kRecLterm]);
         lw += amb ? 0.0 : t;
     }
     return zi;
@@ -1097,17 +1148,15 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         // Ca, Cb, c', 1/R_ii (record slots 21..24) in two 16-byte LDS reads
                         static_assert(kSzCa == 21 && kSzCb == 22 && kRecCp == 23 && kRecIrii == 24, "record layout");
                         typedef double d2v __attribute__((ext_vector_type(2)));
-                        const d2v r22 = ((const __attribute__((address_space(3))) d2v*)rec)[11];
-                        const d2v r24 = ((const __attribute__((address_space(3))) d2v*)rec)[12];
-                        const double rca = rec[kSzCa];
-                        const double mu = (r22[1] - acc[(15 - s) & 15]) * r24[0];
+                        const RecRegs rr = load_rec(rec);
+                        const double mu = (rr[kRecCp] - acc[(15 - s) & 15]) * rr[kRecIrii];
                         LGS_DC_T(t_sz0);
                         // certified decision at the blocked-order mean (the |z| sum
                         // bounded by the cap a.z1cap, checked after the sub-panel); a
                         // decision not covered is a guess, verified after the sub-panel
                         bool un;
-                        const double zi = decide_coord_rec<WL, true, LIBM>(a, i, mu, rec, rs, lw, flags, etab_s,
-                                                                     cert_dmu(rca, r22[0], a.z1cap, mu),
+                        const double zi = decide_coord_rec<WL, true, LIBM>(a, i, mu, rec, rr, rs, lw, flags, etab_s,
+                                                                     cert_dmu(rr[kSzCa], rr[kSzCb], a.z1cap, mu),
                                                                      un);
                         if (un) cert_fl[threadIdx.x] |= 1 << s;
 #ifdef LGS_DIAG_CYCLES
@@ -1128,9 +1177,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         }
                         if constexpr (OZ)
                             if (!(zi <= 32639.0 && zi >= -32767.0)) flags |= kFlagOverflow16;
-                        const lds_cdptr rc = rec + kRecRs;
 #pragma unroll
-                        for (int k = 0; k < 15; ++k) acc[(k - s) & 15] = fma(rc[14 - k], zi, acc[(k - s) & 15]);
+                        for (int k = 0; k < 15; ++k) acc[(k - s) & 15] = fma(rr[kRecRs + 14 - k], zi, acc[(k - s) & 15]);
                         acc[(15 - s) & 15] = 0.0;  // the next step's logical acc[0]
                     }
                 }
@@ -1222,14 +1270,12 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
                     const lds_cdptr rec = (lds_cdptr)rec_lds + (i - (p_hi - 32)) * kRecStride;
                     static_assert(kSzCa == 21 && kSzCb == 22 && kRecCp == 23 && kRecIrii == 24, "record layout");
-                    const d2v r22 = ((const __attribute__((address_space(3))) d2v*)rec)[11];
-                    const d2v r24 = ((const __attribute__((address_space(3))) d2v*)rec)[12];
-                    const double rca = rec[kSzCa];
-                    const double mu = (r22[1] - acc[15]) * r24[0];
+                    const RecRegs rr = load_rec(rec);
+                    const double mu = (rr[kRecCp] - acc[15]) * rr[kRecIrii];
                     LGS_DC_T(t_sz0);
                     bool un;
-                    const double zi = decide_coord_rec<WL, true, LIBM>(a, i, mu, rec, rs, lw, flags, etab_s,
-                                                                       cert_dmu(rca, r22[0], a.z1cap, mu), un);
+                    const double zi = decide_coord_rec<WL, true, LIBM>(a, i, mu, rec, rr, rs, lw, flags, etab_s,
+                                                                       cert_dmu(rr[kSzCa], rr[kSzCb], a.z1cap, mu), un);
                     flm |= un ? (1 << s) : 0;
 #ifdef LGS_DIAG_CYCLES
                     {
@@ -1264,9 +1310,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         pnz |= zi != 0.0;
                     }
                     z1e += fabs(zi);
-                    const lds_cdptr rc = rec + kRecRs;
 #pragma unroll
-                    for (int k = 14; k >= 0; --k) acc[k + 1] = fma(rc[14 - k], zi, acc[k]);
+                    for (int k = 14; k >= 0; --k) acc[k + 1] = fma(rr[kRecRs + 14 - k], zi, acc[k]);
                     acc[0] = 0.0;
                 }
                 if constexpr (OZ) {
