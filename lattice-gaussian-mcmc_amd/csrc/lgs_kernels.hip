@@ -812,6 +812,9 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
         v4i32_t pf[4];
         v4u_t w[NG][2];
         auto hist_load = [&](int ch) {
+#ifdef LGS_DIAG_HIST_FIXED  // diagnostic builds only (NOT bit-exact): every chunk reads chunk 0's history
+            ch = 0;
+#endif
             const v4u_t* h0 = (const v4u_t*)(hb0 + (size_t)ch * hstep);
             const v4u_t* h1 = (const v4u_t*)(hb1 + (size_t)ch * hstep);
             w[0][0] = *(h0);
