@@ -186,12 +186,16 @@ int run_bz_fp64(lgs_ctx* c, const BzCall& b);
 // Wait for the stream; if an int8-digit B z saw a coefficient beyond two digits,
 // replay the pending B z launches with the fp64 kernel.  Must run before any
 // copy that consumes their output.
-int settle_bz(lgs_ctx* c) {
-    HIP_TRY(hipStreamSynchronize(c->stream));
+// f0_known: the caller has synchronised and read flag word 0 already (*f0_known).
+int settle_bz(lgs_ctx* c, const unsigned int* f0_known = nullptr) {
+    if (!f0_known) HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->pending_i8.empty()) return LGS_OK;
     {
         unsigned int f0 = 0;
-        HIP_TRY(hipMemcpy(&f0, c->flags.p, sizeof(f0), hipMemcpyDeviceToHost));
+        if (f0_known)
+            f0 = *f0_known;
+        else
+            HIP_TRY(hipMemcpy(&f0, c->flags.p, sizeof(f0), hipMemcpyDeviceToHost));
         if (f0 & lgs::kFlagI8Range) {  // coefficients beyond two int8 digits: redo in fp64
             for (const auto& b : c->pending_i8) {
                 int rc = run_bz_fp64(c, b);
@@ -229,8 +233,10 @@ void fold_counters(lgs_ctx* c, const unsigned int* fw) {
     }
 }
 
-int finish(lgs_ctx* c) {  // sync, fold timers, report kernel flags
-    int rc0 = settle_bz(c);
+// fw_known: the caller has synchronised and read the flag words (one device-to-host
+// copy per call instead of one per check: each is a round trip the GPU idles through).
+int finish(lgs_ctx* c, const unsigned int* fw_known = nullptr) {  // sync, fold timers, report kernel flags
+    int rc0 = settle_bz(c, fw_known);
     if (rc0) return rc0;
     for (auto& t : c->pending) {
         float ms = 0;
@@ -243,14 +249,16 @@ int finish(lgs_ctx* c) {  // sync, fold timers, report kernel flags
     }
     c->pending.clear();
     unsigned int fw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    HIP_TRY(hipMemcpy(fw, c->flags.p, sizeof(fw), hipMemcpyDeviceToHost));
+    if (fw_known)
+        memcpy(fw, fw_known, sizeof(fw));
+    else
+        HIP_TRY(hipMemcpy(fw, c->flags.p, sizeof(fw), hipMemcpyDeviceToHost));
     const unsigned int f = fw[0];
     c->resolved_seen = 0;
-    if (fw[1] || fw[2] || fw[3]) {
+    if (fw[1] || fw[2] || fw[3])
         fold_counters(c, fw);
-        const unsigned int zero[5] = {0, 0, 0, 0, 0};
-        HIP_TRY(hipMemcpy((unsigned int*)c->flags.p + 1, zero, sizeof(zero), hipMemcpyHostToDevice));
-    }
+    if (fw[1] || fw[2] || fw[3] || fw[4] || fw[5])  // ordered before the next launches on the stream
+        HIP_TRY(hipMemsetAsync((unsigned int*)c->flags.p + 1, 0, 5 * sizeof(unsigned int), c->stream));
     if (f & lgs::kFlagNonFinite)
         return fail(LGS_ERR_NONFINITE, "non-finite conditional mean (reference raises ValueError)");
     if (f & lgs::kFlagOverflow)
@@ -270,7 +278,7 @@ int finish_or_redo(lgs_ctx* c, bool oz_used, int& zb, bool& redo) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     unsigned int fw[8];
     HIP_TRY(hipMemcpy(fw, c->flags.p, sizeof(fw), hipMemcpyDeviceToHost));
-    if (!(fw[0] & lgs::kAbortMask)) return finish(c);
+    if (!(fw[0] & lgs::kAbortMask)) return finish(c, fw);
     c->pending_i8.clear();
     for (auto& t : c->pending) {  // the aborted attempt's timers are not kept
         c->pool.push_back(t.a);

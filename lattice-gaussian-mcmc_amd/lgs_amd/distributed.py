@@ -128,17 +128,26 @@ class LagSums:
         self.n = 0
 
     def update(self, x):
-        torch, L, h = self.t, self.L, self.have
-        nc, T = x.shape
+        self.update_device(x)
+        self.update_host(*x.shape)
+
+    def update_device(self, x):
+        """The device part: sums and ring updated in place (graph-capturable)."""
+        torch, L = self.t, self.L
+        T = x.shape[1]
         xs = torch.cat([self.ring, x], 1)                      # (nc, L + T)
         win = xs.unfold(1, T, 1).flip(1)                       # win[:, k] = xs[:, L - k : L - k + T]
         self.S += (win * x[:, None, :]).sum((0, 2))
-        k = np.arange(L + 1)
-        self.N += nc * np.maximum(T - np.maximum(k - h, 0), 0)
         self.S1 += x.sum()
-        self.n += x.numel()
-        self.ring = xs[:, T:].clone() if T < L else x[:, T - L:].clone()
-        self.have = min(L, h + T)
+        self.ring.copy_(xs[:, T:] if T < L else x[:, T - L:])
+
+    def update_host(self, nc, T):
+        """The host part: pair counts (the ring starts as zeros, so pairs reaching
+        before the first step add nothing to S but must not be counted)."""
+        k = np.arange(self.L + 1)
+        self.N += nc * np.maximum(T - np.maximum(k - self.have, 0), 0)
+        self.n += nc * T
+        self.have = min(self.L, self.have + T)
 
     def parts(self):
         t = self.t
@@ -175,6 +184,13 @@ class StreamingShard:
         self.lags = lags
         self.binv = torch.as_tensor(np.asarray(binv_row, dtype=np.float64)).to(device)
         self.next_step = first_step
+        # the per-block lag-sum update is ~20 small kernels; on a GPU it is replayed
+        # as one captured graph from the second block on (the host would otherwise
+        # launch them one by one after lgs_imhk's final synchronisation, with the
+        # GPU idle in between).  LGS_NO_GRAPH=1: eager.
+        self._graph = None
+        self._graph_key = None
+        self._graph_ok = str(device).startswith("cuda") and os.environ.get("LGS_NO_GRAPH", "0") != "1"
         self.reset_stats()
 
     def reset_stats(self):
@@ -184,15 +200,39 @@ class StreamingShard:
         self.lag_z = LagSums(t, self.lag_chains, self.lags, t.int64, self.dev)
         self.lag_v = LagSums(t, self.lag_chains, self.lags, t.float64, self.dev)
         self.steps_done = 0
+        self._graph = None  # captured against the previous sums' buffers
 
     def step(self, n_steps: int):
         v = self.advance(self.next_step, n_steps, self.acc, self.mom)
         self.next_step += n_steps
         self.steps_done += n_steps
         if v is not None:
-            vs = v[:self.lag_chains]
-            self.lag_z.update(self.t.round(vs @ self.binv).long())
-            self.lag_v.update((vs * vs).sum(-1) * 1e-6)
+            self._lag_update(v)
+            self.lag_z.update_host(self.lag_chains, n_steps)
+            self.lag_v.update_host(self.lag_chains, n_steps)
+
+    def _lag_device(self, v):
+        vs = v[:self.lag_chains]
+        self.lag_z.update_device(self.t.round(vs @ self.binv).long())
+        self.lag_v.update_device((vs * vs).sum(-1) * 1e-6)
+
+    def _lag_update(self, v):
+        t = self.t
+        key = (v.data_ptr(), tuple(v.shape))
+        if not self._graph_ok:
+            self._lag_device(v)
+        elif self._graph is not None and self._graph_key == key:
+            self._graph.replay()
+        elif self._graph_key == key:  # second block on the same buffer: capture, then replay
+            g = t.cuda.CUDAGraph()
+            with t.cuda.graph(g):
+                self._lag_device(v)
+            self._graph = g
+            g.replay()
+        else:  # first block (or a new buffer): eager, which also warms the kernels up
+            self._graph = None
+            self._graph_key = key
+            self._lag_device(v)
 
     def reduce(self, group=None) -> dict:
         """One all-reduce of [accepts, moments, lag sums of both functionals]."""
