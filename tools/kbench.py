@@ -43,6 +43,12 @@ def run_one(args):
     avg = ms / k
     out = {"lib": os.environ.get("LGS_LIB", "default"), "config": args.config, "d": d, "n": n,
            "kernel_ms": round(avg, 3), "samples_per_s": round(n / avg * 1e3, 1)}
+    if args.hash:  # outputs of the last launch, for A/B equality of library variants
+        import hashlib
+        torch.cuda.synchronize()
+        out["z_sha"] = hashlib.sha256(z.cpu().numpy().tobytes()).hexdigest()[:16]
+        if v is not None:
+            out["v_sha"] = hashlib.sha256(v.cpu().numpy().tobytes()).hexdigest()[:16]
     if args.bz:
         ms, k = ctx.timing_get(_capi.KERNEL_BZ)
         out["bz_ms"] = round(ms / k, 3)
@@ -73,6 +79,7 @@ if __name__ == "__main__":
     ap.add_argument("--exact", action="store_true")
     ap.add_argument("--one", action="store_true")
     ap.add_argument("--bz", action="store_true", help="also compute v = Bz and time bz_i8")
+    ap.add_argument("--hash", action="store_true", help="print sha256 prefixes of the last launch's z (and v)")
     args = ap.parse_args()
     libs = os.environ.get("LGS_LIBS")
     if args.one or not libs:
