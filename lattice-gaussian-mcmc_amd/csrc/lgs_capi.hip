@@ -740,6 +740,14 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
         std::copy(rsv.data() + i * 15, rsv.data() + i * 15 + 15, r + lgs::kRecRs);
         r[lgs::kRecScale] = rscale[i];
     }
+    for (int64_t top = d; top >= 16; top -= 16) {  // whole 16-row sub-panels (top = d - 16 sp)
+        bool all = true;
+        for (int64_t i = top - 16; i < top && all; ++i) {
+            const double* r = crec.data() + i * lgs::kRecStride;
+            all = r[0] != 0.0 && (int)r[2] == lgs::kSzSmall && r[7] == 0.0;
+        }
+        for (int64_t i = top - 16; i < top; ++i) crec[i * lgs::kRecStride + lgs::kRecSpec] = all ? 1.0 : 0.0;
+    }
     c->has_rd = oz;
     if (oz) {
         if ((rc = c->RD.reserve(rdv.size())) || (rc = c->RDOFF.reserve(rdoff.size() * 8))) return rc;

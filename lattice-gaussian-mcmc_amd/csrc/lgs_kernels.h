@@ -53,6 +53,10 @@ constexpr int kRecCp = kSzUsed, kRecIrii = kSzUsed + 1, kRecRos = kSzUsed + 2,
 // int8-digit far field (klein_mfma_kernel OZ): row scale 2^E_i of the
 // coordinate's row over its panel's far columns
 constexpr int kRecScale = kRecRs + 15;
+// 1.0 when the coordinate's 16-row sub-panel is whole and all its coordinates are
+// of the small kind with one dominant window point possible (q[7] == 0): the
+// sub-panel is then decided speculatively in parallel (klein_mfma_kernel)
+constexpr int kRecSpec = kRecScale + 1;
 constexpr int kRecStride = kRecRs + 18;  // 46: 368 bytes, 16-byte multiple
 // int8-digit far field layout: per 32-row panel pk >= 1 (K = 32 pk far columns,
 // ceil(K/64) chunks of 64): [chunk][row tile t][digit a][lane][16 bytes]

@@ -1340,12 +1340,22 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
             };
             // one copy of the 16-step near field for both sub-panels (a second inlined
             // copy doubles the hot loop's code beyond the instruction cache)
+            bool upper_zero = false;  // the upper sub-panel was kept speculatively: all its z are 0
 #pragma nounroll
             for (int half = 0; half < 2; ++half) {
                 const int top = p_hi - 16 * half;
                 const int rows16 = top < 16 ? top : 16;
                 if (rows16 <= 0) break;
-                if (half == 1) {
+                if (half == 1 && upper_zero) {
+                    // the coupling R[L rows, U cols] z_U is exactly +0 (z_U = 0; the MFMA
+                    // sums of +-0 products from +0 stay +0), and F + 0 = F: skip it
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[r] = F[r * LDF + lane];
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                } else if (half == 1) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     d4_t c[4];
@@ -1373,6 +1383,51 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                 }
+#ifndef LGS_NO_SPEC
+                // Speculative sub-panel (host flag kRecSpec: 16 coordinates of the small
+                // kind, e.g. the q-coordinates of NTRU / q-ary bases, whose sigma_i ~ 1e-2
+                // make z = rint(mu) = 0 all but always): decided all at once assuming every
+                // earlier z of the sub-panel is 0.  With those z = 0 the sequential form's
+                // FMAs leave the running sums bit-for-bit unchanged (fma(r, +-0, a) = a; a
+                // is never -0), so each mean -- hence each decision and weight term -- is
+                // exactly the sequential one.  Kept only when every lane's 16 decisions are
+                // certified one-dominant-point decisions (no draw) with z = 0; otherwise the
+                // sub-panel is redone sequentially from the untouched sums.
+                if (rows16 == 16 &&
+                    __builtin_amdgcn_readfirstlane(
+                        (int)((lds_cdptr)rec_lds)[(top - 1 - (p_hi - 32)) * kRecStride + kRecSpec]) == 1) {
+                    double term[16];
+                    bool ok = true;
+#pragma unroll
+                    for (int s = 0; s < 16; ++s) {
+                        const lds_cdptr rec = (lds_cdptr)rec_lds + (top - 1 - s - (p_hi - 32)) * kRecStride;
+                        const double mu = (rec[kRecCp] - acc[15 - s]) * rec[kRecIrii];
+                        const double is = rec[1], is2 = is * is;
+                        const double c = rint(mu), d1 = fabs(mu - c), t = d1 * is;
+                        const double emax = -0.5 * (t * t);
+                        const double gap = 0.5 * is2 * (1.0 - 2.0 * d1);
+                        const double hl = ceil(mu + rec[6]) - floor(mu - rec[6]);
+                        const double dmu = cert_dmu(rec[kSzCa], rec[kSzCb], a.z1cap, mu);
+                        const bool fast = gap > 745.2 && !(a.linear_probs && emax < -745.2) &&
+                                          gap - 745.2 > 1.01 * dmu * hl * is2 + 1e-12 * gap;
+                        ok = ok && isfinite(mu) && fast && c == 0.0;
+                        term[s] = WL ? emax : ref_weight(c, mu, rec[kRecRos], rec[kRecIsr], rec[kRecLterm]);
+                    }
+                    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+#pragma unroll
+                        for (int s = 0; s < 16; ++s) lw += term[s];  // the sequential order
+#pragma unroll
+                        for (int s = 0; s < 16; ++s) Z[(size_t)(top - 1 - s) * ldz + p] = (ZT)0;
+                        if constexpr (OZ) {  // int16 history: z + 128 in all 16 positions
+                            v4u_t* hp4 = (v4u_t*)(a.h16 + ((size_t)((top - 16 + a.h16_shift) >> 4) * a.h16_lanes + p) * 16);
+                            hp4[0] = (v4u_t){0x00800080u, 0x00800080u, 0x00800080u, 0x00800080u};
+                            hp4[1] = (v4u_t){0x00800080u, 0x00800080u, 0x00800080u, 0x00800080u};
+                        }
+                        upper_zero = true;
+                        continue;
+                    }
+                }
+#endif
 #ifdef LGS_NEAR_UNROLLED
                 near16(rows16, top);
 #else

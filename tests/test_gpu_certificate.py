@@ -43,3 +43,46 @@ def test_default_order_equals_exact_order_at_scale(capi, oracle, cfg, n):
     bad = int((za != zb).any(dim=0).sum())
     print(f"{cfg}: {n} samples, {redos} certificate replays, {bad} samples differ")
     assert bad == 0
+
+
+@pytest.mark.parametrize("cfg,center_scale", [("C3_ntru512", 0.0), ("C3_ntru512", 3e4), ("C4_qary1024", 0.0),
+                                              ("C4_qary1024", 3e4)])
+def test_speculative_small_kind_subpanels(capi, oracle, cfg, center_scale):
+    """Sub-panels of tiny-sigma coordinates (the q-coordinates) are decided all at
+    once on the speculation that every z of the sub-panel is 0 (kRecSpec): kept
+    when it holds in the whole wave, else redone in order.  Center 0: the
+    speculation holds (z = 0 there); a center of scale ~q moves those means off 0,
+    so the redo path runs.  Both must equal the reference-order kernel: z exactly,
+    the log weights to rounding (their terms use the blocked-order means).  That the
+    kept speculation reproduces the sequential default kernel bit for bit (z and log
+    weights) is checked across builds (LGS_NO_SPEC) with tools/kbench.py --hash
+    (profiles/r03v_*)."""
+    import torch
+    from lgs_amd.lattices import build_config
+    lat, sigma = build_config(cfg)
+    B = lat.basis
+    d = B.shape[0]
+    rng = np.random.default_rng(5)
+    center = rng.uniform(-center_scale, center_scale, d) if center_scale else None
+    R, cp = oracle.qr_prepare(B, center)
+    ctx = capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    n = 1 << 14
+    za = torch.empty((d, n), dtype=torch.int32, device="cuda")
+    zb = torch.empty_like(za)
+    la = torch.empty(n, dtype=torch.float64, device="cuda")
+    lb = torch.empty_like(la)
+    f = capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR
+    ctx.klein(91, 0, n, za, None, la, f)
+    ctx.klein(91, 0, n, zb, None, lb, f | capi.LGS_EXACT_ORDER)
+    torch.cuda.synchronize()
+    small = torch.as_tensor(np.flatnonzero(sigma / np.diag(R) < 4.0), device="cuda")  # the q-coordinates
+    assert small.numel() >= d // 4
+    nz_q = int((za[small] != 0).any(dim=0).sum())
+    print(f"{cfg} center {center_scale}: samples with a nonzero q-coordinate: {nz_q} of {n}")
+    if center_scale == 0.0:
+        assert nz_q == 0
+    else:
+        assert nz_q > n // 2
+    assert int((za != zb).any(dim=0).sum()) == 0
+    assert torch.allclose(la, lb, rtol=1e-10, atol=1e-9)

@@ -47,6 +47,7 @@ def run_one(args):
         import hashlib
         torch.cuda.synchronize()
         out["z_sha"] = hashlib.sha256(z.cpu().numpy().tobytes()).hexdigest()[:16]
+        out["lw_sha"] = hashlib.sha256(lw.cpu().numpy().tobytes()).hexdigest()[:16]
         if v is not None:
             out["v_sha"] = hashlib.sha256(v.cpu().numpy().tobytes()).hexdigest()[:16]
     if args.bz:
