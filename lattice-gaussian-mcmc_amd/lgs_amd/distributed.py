@@ -214,7 +214,10 @@ class StreamingShard:
     def _lag_device(self, v):
         vs = v[:self.lag_chains]
         self.lag_z.update_device(self.t.round(vs @ self.binv).long())
-        self.lag_v.update_device((vs * vs).sum(-1) * 1e-6)
+        # ||v||^2 in one fused multiply-reduce pass over v (no v*v temporary); v is
+        # integer, so every partial sum is an exact integer below 2^53 and the result
+        # equals (v * v).sum(-1) in any summation order
+        self.lag_v.update_device(self.t.linalg.vecdot(vs, vs) * 1e-6)
 
     def _lag_update(self, v):
         t = self.t
