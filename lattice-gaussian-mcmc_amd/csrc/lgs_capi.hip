@@ -107,6 +107,7 @@ struct lgs_ctx {
     DevBuf RD, RDOFF;             // int8-digit far field: R digit fragments, panel offsets
     bool has_rd = false, oz_off = false;  // oz_off: a |z| > 32767 was seen (sticky)
     DevBuf H16, F0;               // int8-digit far field scratch: coefficient history, tile-0 sums
+    DevBuf ZNZ;                   // per history block and lane: any nonzero z (B z's chunk skipping)
     // the last Klein launch's history, valid for columns [0, cols) of the store Z it
     // wrote (B z reads its digits from there); reset by every Klein launch
     struct {
@@ -361,6 +362,8 @@ int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int zb, void* 
         const int64_t blocks = (c->d + shift) / 16 + 5;  // + one 64-column chunk of padding
         int rc = c->H16.reserve((size_t)blocks * lanes * 32);
         if (rc) return rc;
+        if ((rc = c->ZNZ.reserve((size_t)blocks * lanes))) return rc;
+        a.znz = c->ZNZ.as<uint8_t>();
         a.rd = c->RD.as<int8_t>();
         a.rd_off = c->RDOFF.as<int64_t>();
         a.h16 = c->H16.as<int16_t>();
@@ -445,7 +448,7 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
                                (int)c->bd_cols, (int)c->d, n, V, c->d, b.rb,
                                b.rstride, b.roff, c->flags.as<unsigned int>(),
                                after_klein && c->hist.Z == Z && Z ? c->H16.as<int16_t>() : nullptr, c->hist.lanes,
-                               c->hist.cols, c->stream, abort));
+                               c->hist.cols, c->stream, abort, c->ZNZ.as<uint8_t>()));
     c->pending_i8.push_back(b);
     return LGS_OK;
 }

@@ -121,6 +121,8 @@ struct KleinArgs {
     int16_t* h16;            // coefficient history, [(i + h16_shift)/16][lane][16] int16
     int h16_shift;           // (16 - d % 16) % 16
     int64_t h16_lanes;       // lanes per 16-coordinate block (>= n)
+    uint8_t* znz;            // nullable (with h16): [(i + h16_shift)/16][lane] 1 when the lane's z of
+                             // that block has a nonzero (B z skips chunks that are all zero)
     const double* rx;    // per 32-row panel: 16x16 block R[p_hi-32.., p_hi-16..] as MFMA A fragments
     const unsigned int* gate;  // nullable: when *gate == 0 every block returns at once (initial draws
                                // of lgs_imhk when no chain needs one, decided on the device)
@@ -242,7 +244,7 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
-                 hipStream_t st, const unsigned int* abort = nullptr);
+                 hipStream_t st, const unsigned int* abort = nullptr, const uint8_t* znz = nullptr);
 // ---- decoding
 // V (row-major n x d) = rows s: sum_c MT[c][r] X[c][s], X coordinate-major fp64 (fp64 MFMA)
 hipError_t gemm_f64(const double* X, int64_t ldx, const double* MT, int d, int64_t n, double* V,

@@ -1244,6 +1244,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     flags = vo.flags;
                     if constexpr (OZ) pnz |= vo.nz != 0;
                 }
+                if constexpr (OZ)  // (this variant keeps no per-sub-panel flag: the block counts as nonzero)
+                    if (a.znz) a.znz[(size_t)((top - 1 + a.h16_shift) >> 4) * a.h16_lanes + p] = 1;
             };
 #endif
             // Rolled near field (default): one loop iteration per coordinate with the
@@ -1264,6 +1266,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
 #pragma unroll
                 for (int j = 0; j < 8; ++j) hp[j] = 0u;
                 int flm = 0;
+                bool snz = false;  // (OZ) a nonzero z in this sub-panel, this lane
                 typedef double d2v __attribute__((ext_vector_type(2)));
 #ifndef LGS_NEAR_UNROLL  // coordinates per loop iteration (the running sums shift by one per step)
 #define LGS_NEAR_UNROLL 1
@@ -1310,7 +1313,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                             const int ih = i + a.h16_shift;
                             a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] = (int16_t)hv;
                         }
-                        pnz |= zi != 0.0;
+                        snz |= zi != 0.0;
                     }
                     z1e += fabs(zi);
 #pragma unroll
@@ -1335,7 +1338,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                                                                  &cert_lds[1][w64], &cert_lds[2][w64], flags);
                     lw = vo.lw;
                     flags = vo.flags;
-                    if constexpr (OZ) pnz |= vo.nz != 0;
+                    if constexpr (OZ) snz |= vo.nz != 0;
+                }
+                if constexpr (OZ) {
+                    pnz |= snz;
+                    if (a.znz) a.znz[(size_t)((top - 1 + a.h16_shift) >> 4) * a.h16_lanes + p] = snz ? 1 : 0;
                 }
             };
             // one copy of the 16-step near field for both sub-panels (a second inlined
@@ -1423,6 +1430,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                             hp4[0] = (v4u_t){0x00800080u, 0x00800080u, 0x00800080u, 0x00800080u};
                             hp4[1] = (v4u_t){0x00800080u, 0x00800080u, 0x00800080u, 0x00800080u};
                         }
+                        if (OZ && a.znz) a.znz[(size_t)((top - 1 + a.h16_shift) >> 4) * a.h16_lanes + p] = 0;
                         upper_zero = true;
                         continue;
                     }
@@ -1965,7 +1973,8 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
                                                     int64_t rb, int64_t rstride, int64_t roff,
                                                     unsigned int* flags, int tx_count, int64_t ty_count,
                                                     const int16_t* __restrict__ h16, int64_t h16_lanes,
-                                                    int64_t hcols, const unsigned int* abort) {
+                                                    int64_t hcols, const unsigned int* abort,
+                                                    const uint8_t* __restrict__ znz) {
     if (aborted(abort)) return;  // (whole grid) the selections were not written
     constexpr int TA = LGS_BZ_TA;  // 32-sample MFMA tiles per wave
     constexpr int BM = 64 * TA, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
@@ -2008,7 +2017,27 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
 #else
     const int ci1 = koff[tx + 1];
 #endif
+    // Chunks where every sample of the tile has z = 0 on all 64 coordinates contribute
+    // exactly nothing: skipped.  The Klein launch that wrote the history flags each
+    // (16-coordinate block, sample) holding a nonzero (znz); thread (zm, zq) checks
+    // block zq of each chunk for its sample, the tile ORs them in LDS.  Samples read
+    // from the coefficient store (not that launch's) count as nonzero.  (NTRU / q-ary
+    // bases: the q-coordinates' z are 0, which leaves ~1 of 6 chunks per tile.)
+    const bool use_znz = KPT == 16 && h16 != nullptr && znz != nullptr;
+    __shared__ unsigned int livew[kOzMaxD / 64 / 32];
+    if (use_znz) {
+        const bool hp = zs_ < n && zcol < hcols;
+        for (int w = tid; w < (ci1 - ci0 + 31) / 32; w += 256) livew[w] = 0u;
+        __syncthreads();
+        for (int ci = ci0; ci < ci1; ++ci) {
+            const int c0 = kchunk[ci] * KC;
+            const bool nz = zs_ < n && (!hp || znz[(size_t)((c0 + zq * 16) >> 4) * h16_lanes + zcol] != 0);
+            if (nz) atomicOr(&livew[(ci - ci0) >> 5], 1u << ((ci - ci0) & 31));
+        }
+        __syncthreads();
+    }
     for (int ci = ci0; ci < ci1; ++ci) {
+        if (use_znz && !((livew[(ci - ci0) >> 5] >> ((ci - ci0) & 31)) & 1u)) continue;  // (uniform)
         const int c0 = kchunk[ci] * KC;
         if (KPT == 16 && h16 != nullptr && zs_ < n && zcol < hcols) {
             // column written by the Klein launch whose int16 history (z + 128,
@@ -2369,13 +2398,17 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
-                 hipStream_t st, const unsigned int* abort) {
+                 hipStream_t st, const unsigned int* abort, const uint8_t* znz) {
     if (n <= 0) return hipSuccess;
-    if (d % 16 != 0 || LGS_BZ_TA != 1) h16 = nullptr;  // history blocks must align with the chunks
+    if (d % 16 != 0 || LGS_BZ_TA != 1 || d > kOzMaxD) h16 = nullptr;  // history blocks must align with the chunks
+#ifdef LGS_BZ_NO_ZNZ
+    znz = nullptr;
+#endif
+    if (h16 == nullptr) znz = nullptr;
     const int tx = ((d + 127) / 128 + LGS_BZ_TXPER - 1) / LGS_BZ_TXPER;  // coordinate-tile groups
     const int64_t ty = (n + 64 * LGS_BZ_TA - 1) / (64 * LGS_BZ_TA);
     const dim3 grid((unsigned)(tx * ((ty + 7) / 8) * 8));  // whole rounds of 8 XCDs (extra tiles exit)
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort, znz));
     return hipGetLastError();
 }
 

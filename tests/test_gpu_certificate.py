@@ -45,15 +45,17 @@ def test_default_order_equals_exact_order_at_scale(capi, oracle, cfg, n):
     assert bad == 0
 
 
-@pytest.mark.parametrize("cfg,center_scale", [("C3_ntru512", 0.0), ("C3_ntru512", 3e4), ("C4_qary1024", 0.0),
-                                              ("C4_qary1024", 3e4)])
-def test_speculative_small_kind_subpanels(capi, oracle, cfg, center_scale):
+@pytest.mark.parametrize("cfg,center_scale,wl", [("C3_ntru512", 0.0, False), ("C3_ntru512", 3e4, False),
+                                                 ("C4_qary1024", 0.0, False), ("C4_qary1024", 3e4, False),
+                                                 ("C3_ntru512", 0.0, True), ("C3_ntru512", 3e4, True)])
+def test_speculative_small_kind_subpanels(capi, oracle, cfg, center_scale, wl):
     """Sub-panels of tiny-sigma coordinates (the q-coordinates) are decided all at
     once on the speculation that every z of the sub-panel is 0 (kRecSpec): kept
     when it holds in the whole wave, else redone in order.  Center 0: the
     speculation holds (z = 0 there); a center of scale ~q moves those means off 0,
     so the redo path runs.  Both must equal the reference-order kernel: z exactly,
-    the log weights to rounding (their terms use the blocked-order means).  That the
+    the log weights to rounding (their terms use the blocked-order means), in
+    reference mode and with Wang-Ling weights.  That the
     kept speculation reproduces the sequential default kernel bit for bit (z and log
     weights) is checked across builds (LGS_NO_SPEC) with tools/kbench.py --hash
     (profiles/r03v_*)."""
@@ -72,7 +74,7 @@ def test_speculative_small_kind_subpanels(capi, oracle, cfg, center_scale):
     zb = torch.empty_like(za)
     la = torch.empty(n, dtype=torch.float64, device="cuda")
     lb = torch.empty_like(la)
-    f = capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR
+    f = capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR | (capi.LGS_WANG_LING if wl else 0)
     ctx.klein(91, 0, n, za, None, la, f)
     ctx.klein(91, 0, n, zb, None, lb, f | capi.LGS_EXACT_ORDER)
     torch.cuda.synchronize()
@@ -85,4 +87,15 @@ def test_speculative_small_kind_subpanels(capi, oracle, cfg, center_scale):
     else:
         assert nz_q > n // 2
     assert int((za != zb).any(dim=0).sum()) == 0
-    assert torch.allclose(la, lb, rtol=1e-10, atol=1e-9)
+    dif = (la - lb).abs()
+    rel = float((dif / lb.abs().clamp_min(1.0)).max())
+    print(f"  log weights: max difference {float(dif.max()):.2e}, relative {rel:.2e}")
+    # Reference mode: the weight terms cancel to rounding.  Wang-Ling: the normaliser
+    # of a sigma_i ~ 1e-3 coordinate moves by |mu - rint(mu)| / sigma_i^2 ~ 1e4 per
+    # unit of mean, and the default kernels' means carry the far field's rounding of R
+    # to 48 bits of its row maximum (covered by the certificate for z, not for the
+    # weight): |dlw| <= 7e-6 at C3 (|lw| up to ~4e3, some samples near 0), DESIGN.md §7
+    if wl:
+        assert float(dif.max()) < 2e-5
+    else:
+        assert rel < 1e-10

@@ -22,13 +22,19 @@ def run_one(args):
     B = lat.basis
     d = B.shape[0]
     Q, R = np.linalg.qr(B)
-    R = np.ascontiguousarray(R * np.where(np.diag(R) < 0, -1.0, 1.0)[:, None])
+    sg = np.where(np.diag(R) < 0, -1.0, 1.0)
+    R = np.ascontiguousarray(R * sg[:, None])
+    cp = np.zeros(d)
+    if args.center:  # c' = Q^T c of a uniform random center of that scale (seed 5)
+        c = np.random.default_rng(5).uniform(-args.center, args.center, d)
+        cp = np.ascontiguousarray((Q * sg[None, :]).T @ c)
     ctx = _capi.Context(0)
-    ctx.set_basis(R, np.zeros(d), B, sigma)
+    ctx.set_basis(R, cp, B, sigma)
     n = args.n
     z = torch.empty((d, n), dtype=torch.int32, device="cuda:0")
     lw = torch.empty(n, dtype=torch.float64, device="cuda:0")
     flags = _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR | (_capi.LGS_EXACT_ORDER if args.exact else 0)
+    flags |= _capi.LGS_WANG_LING if args.wl else 0
     v = torch.empty((n, d), dtype=torch.float64, device="cuda:0") if args.bz else None
     ctx.klein(1, 0, n, z, v, lw, flags)
     import ctypes
@@ -42,6 +48,7 @@ def run_one(args):
     ms, k = ctx.timing_get(_capi.KERNEL_KLEIN)
     avg = ms / k
     out = {"lib": os.environ.get("LGS_LIB", "default"), "config": args.config, "d": d, "n": n,
+           "wl": args.wl, "center": args.center,
            "kernel_ms": round(avg, 3), "samples_per_s": round(n / avg * 1e3, 1)}
     if args.hash:  # outputs of the last launch, for A/B equality of library variants
         import hashlib
@@ -81,6 +88,8 @@ if __name__ == "__main__":
     ap.add_argument("--one", action="store_true")
     ap.add_argument("--bz", action="store_true", help="also compute v = Bz and time bz_i8")
     ap.add_argument("--hash", action="store_true", help="print sha256 prefixes of the last launch's z (and v)")
+    ap.add_argument("--wl", action="store_true", help="Wang-Ling weights")
+    ap.add_argument("--center", type=float, default=0.0, help="scale of a random center (0: the origin)")
     args = ap.parse_args()
     libs = os.environ.get("LGS_LIBS")
     if args.one or not libs:
