@@ -1151,9 +1151,13 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
             Scope s(c, 3);
             // carried-in states first: the fused pass overwrites z_state
             HIP_TRY(lgs::launch::moments_carry(zs, ob, cm, nc, (int)d, c->ccnt.as<int32_t>(), mom, c->stream, fl));
+            // the block's Klein launch wrote the int8-digit history of this store: its
+            // per-block nonzero flags let the pass skip all-zero coefficient blocks
+            const bool zflags = c->hist.Z == c->Z.p && c->hist.Z != nullptr;
             HIP_TRY(lgs::launch::moments_final(c->Z.p, zb, ldzb, c->cnt.as<int32_t>(), npb, Tb,
                                                fuse_final ? c->fsel.as<int64_t>() : nullptr, (int)d, mom, zs,
-                                               ob, cm, nc, c->stream, fl));
+                                               ob, cm, nc, c->stream, fl, zflags ? c->ZNZ.as<uint8_t>() : nullptr,
+                                               c->hist.lanes, (int)((16 - d % 16) % 16)));
         }
         if ((z_samples || v_samples) && kb > 0) {
             // kept states q = chain*kb + k, gathered coordinate-major (d x nq); chain-major

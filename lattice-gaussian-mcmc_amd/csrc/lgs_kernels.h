@@ -217,7 +217,8 @@ hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, int z
 // abort (nullable) below: the kernel returns at once when *abort & kAbortMask
 hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int64_t T,
                          const int64_t* fsel, int d, unsigned long long* mom, void* zs, int ob,
-                         int zs_cm, int64_t nc, hipStream_t st, const unsigned int* abort = nullptr);
+                         int zs_cm, int64_t nc, hipStream_t st, const unsigned int* abort,
+                         const uint8_t* znz = nullptr, int64_t zlanes = 0, int zshift = 0);
 hipError_t moments_carry(const void* zs, int zb, int coord_major, int64_t nc, int d,
                          const int32_t* cc, unsigned long long* mom, hipStream_t st,
                          const unsigned int* abort = nullptr);

@@ -1603,7 +1603,9 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
                                                             int d, int64_t chunk,
                                                             unsigned long long* mom,
                                                             OT* __restrict__ zs, int zs_cm, int64_t nc,
-                                                            const unsigned int* abort) {
+                                                            const unsigned int* abort,
+                                                            const uint8_t* __restrict__ znz, int64_t zlanes,
+                                                            int zshift) {
     if (aborted(abort)) return;
     const int i0 = blockIdx.y * RY;
     const int64_t p0 = (int64_t)blockIdx.x * chunk;
@@ -1623,11 +1625,21 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
         typedef ZT zv_t __attribute__((ext_vector_type(VW)));
         typedef int iv4_t __attribute__((ext_vector_type(4)));
         const double rT = 1.0 / (double)T;
+        // (znz: the Klein launch's per-(16-coordinate block, proposal) nonzero flags; the
+        // VW proposals of a load whose blocks are all zero need no coefficient load)
+        const int zb0 = (i0 + zshift) >> 4, zb1 = (i0 + RY - 1 + zshift) >> 4;
         for (int64_t p = p0 + VW * (int64_t)threadIdx.x; p < p1; p += VW * 256) {
             zv_t zv[RY];
+            bool live = true;
+            if (znz != nullptr) {
+                typedef unsigned int u2_t __attribute__((ext_vector_type(2)));
+                const u2_t f0 = *(const u2_t*)(znz + (size_t)zb0 * zlanes + p);
+                const u2_t f1 = *(const u2_t*)(znz + (size_t)zb1 * zlanes + p);
+                live = ((f0[0] | f0[1] | f1[0] | f1[1]) != 0u);
+            }
 #pragma unroll
             for (int r = 0; r < RY; ++r)
-                zv[r] = i0 + r < d ? *(const zv_t*)(Z + (size_t)(i0 + r) * ldz + p) : (zv_t){};
+                zv[r] = live && i0 + r < d ? *(const zv_t*)(Z + (size_t)(i0 + r) * ldz + p) : (zv_t){};
             int w[VW];
 #pragma unroll
             for (int g = 0; g < VW / 4; ++g) {
@@ -2275,8 +2287,13 @@ hipError_t accept(const AcceptArgs& a, hipStream_t st) {
 
 hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int64_t T,
                          const int64_t* fsel, int d, unsigned long long* mom, void* zs, int ob,
-                         int zs_cm, int64_t nc, hipStream_t st, const unsigned int* abort) {
+                         int zs_cm, int64_t nc, hipStream_t st, const unsigned int* abort,
+                         const uint8_t* znz, int64_t zlanes, int zshift) {
     if (n <= 0) return hipSuccess;
+    if (zb != 2 || zlanes % 8 != 0) znz = nullptr;  // (8 proposals per flag load, 16-bit store only)
+#ifdef LGS_MOM_NO_ZNZ
+    znz = nullptr;
+#endif
     const int64_t chunk = 16384;  // multiple of 4
     constexpr int RY = 4;  // rows per workgroup, vector path
     const dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
@@ -2286,9 +2303,9 @@ hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt,
                      (!cnt || ((uintptr_t)cnt % 16) == 0);
     LGS_ZT(zb, ZT, LGS_ZT(ob, OT, {
         if (vec)
-            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, true, RY>), gridv, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort);
+            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, true, RY>), gridv, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort, znz, zlanes, zshift);
         else
-            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, false>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort);
+            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, false>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort, (const uint8_t*)nullptr, (int64_t)0, 0);
     }));
     return hipGetLastError();
 }
