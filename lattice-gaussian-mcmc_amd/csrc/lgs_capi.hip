@@ -615,7 +615,7 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     //    roundings of at most sum_j (|R_ij| + 2^E/256)(|z_j| + 512) with 2^E <= 8 M
     //    -> (2 + 2^(55-8D)) u M Z1 in Cb, 7.1 u (512 L1 + 16 M d) in Ca;
     //  * subtraction, reciprocal / division: 5 u |mu| (the kernels' 6e-16 |mu|).
-    std::vector<double> cert(2 * dd, 0.0);
+    std::vector<double> cert(2 * dd, 0.0), cbc(dd, 0.0);
     {
         const double u = 0x1p-53, g = (2.0 * (double)d + 80.0) * u;
         for (size_t i = 0; i < dd; ++i) {
@@ -630,6 +630,12 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
             const double cb = 1.01 * (1.1 * g / (1.0 - g) + (2.0 + std::ldexp(1.0, 55 - 8 * lgs::kOzDigits)) * u) * M * ir;
             cert[2 * i] = ca;
             cert[2 * i + 1] = cb;
+            // coarse far field (klein_mfma_kernel, reference mode, panels of two
+            // speculative sub-panels): the digits below the kOzCoarse most significant
+            // ones are dropped, |dropped| <= 128 (256^-4 + 256^-5 + 256^-6) 2^E
+            // < 2^(E - 24.99) <= 2^(31.01) u M per unit of z, plus the rounding above
+            cbc[i] = 1.01 * (1.1 * g / (1.0 - g) + (2.0 + std::ldexp(1.0, 55 - 8 * lgs::kOzDigits) +
+                                                    std::ldexp(1.0, 56 - 8 * lgs::kOzCoarse)) * u) * M * ir;
             szc[i * lgs::kSzcStride + lgs::kSzCa] = ca;
             szc[i * lgs::kSzcStride + lgs::kSzCb] = cb;
         }
@@ -742,6 +748,7 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
         r[lgs::kRecLterm] = co[4 * dd + i];
         std::copy(rsv.data() + i * 15, rsv.data() + i * 15 + 15, r + lgs::kRecRs);
         r[lgs::kRecScale] = rscale[i];
+        r[lgs::kRecCbC] = cbc[i];
     }
     for (int64_t top = d; top >= 16; top -= 16) {  // whole 16-row sub-panels (top = d - 16 sp)
         bool all = true;

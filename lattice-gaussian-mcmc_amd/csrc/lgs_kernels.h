@@ -57,7 +57,12 @@ constexpr int kRecScale = kRecRs + 15;
 // of the small kind with one dominant window point possible (q[7] == 0): the
 // sub-panel is then decided speculatively in parallel (klein_mfma_kernel)
 constexpr int kRecSpec = kRecScale + 1;
+// Cb of the certificate for a mean whose far field used only the 3 most significant
+// R digits (reference mode, panels of two speculative sub-panels: klein_mfma_kernel)
+constexpr int kRecCbC = kRecScale + 2;
 constexpr int kRecStride = kRecRs + 18;  // 46: 368 bytes, 16-byte multiple
+static_assert(kRecCbC < kRecStride, "record layout");
+constexpr int kOzCoarse = 4;  // R digits of the far field in coarse panels
 // int8-digit far field layout: per 32-row panel pk >= 1 (K = 32 pk far columns,
 // ceil(K/64) chunks of 64): [chunk][row tile t][digit a][lane][16 bytes]
 #ifndef LGS_OZ_DIGITS

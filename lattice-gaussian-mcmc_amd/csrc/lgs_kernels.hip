@@ -756,7 +756,7 @@ struct ZQuad<int64_t> {
 
 __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_hi, int64_t p0, int lane,
                                              lds_cdptr rec, double* F, int LDF, double (&acc)[16],
-                                             int8_t* ash, const uint32_t* nzm) {
+                                             int8_t* ash, const uint32_t* nzm, bool coarse = false) {
     const int d = a.d;
     const int K = d - p_hi, nch = (K + 63) / 64;
     // chunk ch covers panels pk-1-2ch and pk-2-2ch (panel q: rows d-32(q+1) .. d-32q-1)
@@ -867,6 +867,8 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int dg = 0; dg < kOzDigits; ++dg) {
+                    // coarse (wave-uniform): only the kOzCoarse most significant digits
+                    if (dg >= kOzCoarse && coarse) continue;
                     const v4i32_t av = sl[(t * kOzDigits + dg) * 64];
                     // digit a = dg + 1: class a - 1 with the high x digit, class a with the low
 #pragma unroll
@@ -1017,6 +1019,18 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
             __syncthreads();
             if (!active) continue;
         }
+        // Coarse panel (reference mode, both sub-panels speculative): the far field with
+        // the kOzCoarse most significant R digits, certified with the matching bound
+        // (kRecCbC).  The weights of reference mode do not see the mean (the two squares
+        // of ref_weight cancel to rounding), and the one-dominant-point margin of these
+        // sigma_i ~ 1e-2 coordinates dwarfs the larger bound.
+        bool coarse = false;
+#ifndef LGS_NO_COARSE
+        if constexpr (OZ && PB == 32 && !WL)
+            coarse = p_hi >= 32 &&
+                     __builtin_amdgcn_readfirstlane((int)((lds_cdptr)rec_lds)[31 * kRecStride + kRecSpec]) == 1 &&
+                     __builtin_amdgcn_readfirstlane((int)((lds_cdptr)rec_lds)[15 * kRecStride + kRecSpec]) == 1;
+#endif
         LGS_DC_T(t_far0);
         LGS_DC_ADD(0, t_far0 - t_panel0);
 #ifdef LGS_DIAG_NO_FAR
@@ -1029,7 +1043,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
           if constexpr (OZ && PB == 32) {
-            oz_far_field(a, pk, p_hi, p0, lane, (lds_cdptr)rec_lds, F, LDF, acc, ash, nzm);
+            oz_far_field(a, pk, p_hi, p0, lane, (lds_cdptr)rec_lds, F, LDF, acc, ash, nzm, coarse);
             (void)NT;
           } else {
             d4_t f[NT][4];
@@ -1280,8 +1294,9 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     const double mu = (rr[kRecCp] - acc[15]) * rr[kRecIrii];
                     LGS_DC_T(t_sz0);
                     bool un;
-                    const double zi = decide_coord_rec<WL, true, LIBM>(a, i, mu, rec, rr, rs, lw, flags, etab_s,
-                                                                       cert_dmu(rr[kSzCa], rr[kSzCb], a.z1cap, mu), un);
+                    const double zi = decide_coord_rec<WL, true, LIBM>(
+                        a, i, mu, rec, rr, rs, lw, flags, etab_s,
+                        cert_dmu(rr[kSzCa], coarse ? rec[kRecCbC] : rr[kSzCb], a.z1cap, mu), un);
                     flm |= un ? (1 << s) : 0;
 #ifdef LGS_DIAG_CYCLES
                     {
@@ -1414,7 +1429,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         const double emax = -0.5 * (t * t);
                         const double gap = 0.5 * is2 * (1.0 - 2.0 * d1);
                         const double hl = ceil(mu + rec[6]) - floor(mu - rec[6]);
-                        const double dmu = cert_dmu(rec[kSzCa], rec[kSzCb], a.z1cap, mu);
+                        const double dmu = cert_dmu(rec[kSzCa], coarse ? rec[kRecCbC] : rec[kSzCb], a.z1cap, mu);
                         const bool fast = gap > 745.2 && !(a.linear_probs && emax < -745.2) &&
                                           gap - 745.2 > 1.01 * dmu * hl * is2 + 1e-12 * gap;
                         ok = ok && isfinite(mu) && fast && c == 0.0;
