@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--numpy-samples", type=int, default=24, help="Klein samples per process, NumPy baseline")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dist", action="store_true", help="N = 1 without the one-rank RCCL group")
+    ap.add_argument("--gram-every", type=int, default=1,
+                    help="exact sum z z^T of the chains' states after every k-th bench step (0: off)")
     ap.add_argument("--counters", default=os.environ.get("LGS_COUNTERS_JSON", ""),
                     help="klein_counters.json of a rocprofv3 profile of this command (default: newest in profiles/)")
     return ap.parse_args()
@@ -205,7 +207,8 @@ def main():
     # bench step, lag sums on the device, one all-reduce (tests/test_distributed.py
     # drives the same class with the oracle over gloo, world 2)
     advance = D.gpu_advance(ctx, seed, first_chain, nc, d, dev, flags=flags, block_steps=T, want_v=not args.no_v)
-    shard = D.StreamingShard(advance, nc, d, binv_row=binv_k, device=dev, lag_chains=ACF_CHAINS, lags=ACF_LAGS)
+    shard = D.StreamingShard(advance, nc, d, binv_row=binv_k, device=dev, lag_chains=ACF_CHAINS, lags=ACF_LAGS,
+                             gram_every=args.gram_every)
     z_state = advance.state["z"]
     nacf = shard.lag_chains
     torch.cuda.synchronize()
@@ -244,6 +247,17 @@ def main():
     acceptance = s_acc / proposals
     acf = {"lags": ACF_LAGS, "chains": nacf * world,
            "z_last": D.StreamingShard.acf(stats["lag_z"]), "norm_v_sq": D.StreamingShard.acf(stats["lag_v"])}
+    covariance = None
+    if args.gram_every:
+        # empirical covariance of the thinned kept states (base.py:154-160) from the
+        # exact all-reduced sums; the checksum is of the int64 sum z z^T itself
+        import hashlib
+        G = stats["gram"][0].cpu().numpy()
+        cov = D.StreamingShard.covariance(stats["gram"])
+        covariance = {"states": int(stats["gram"][2][0].item()), "every_steps": args.gram_every * T,
+                      "sum_zzT_sha256": hashlib.sha256(np.ascontiguousarray(G).tobytes()).hexdigest()[:16],
+                      "trace": float(np.trace(cov)), "offdiag_abs_max": float(np.abs(cov - np.diag(np.diag(cov))).max()),
+                      "diag_min": float(np.diag(cov).min()), "diag_max": float(np.diag(cov).max())}
 
     # ---- parity: the timed run's final chain states against the oracle.  In the
     # reference's IMHK mode every proposal is accepted (the weight is a constant up to
@@ -287,18 +301,26 @@ def main():
         roofline["counters_note"] = f"newest profile {cnt_path} is of another library build: not used"
     if cnt and cnt.get("units_per_launch") == units:
         f64 = cnt["fp64_flops"]
+        # every fraction divides the profiled run's counters by THAT run's own kernel
+        # duration (rocprofv3 kernel trace of the same command); this run's HIP-event
+        # time is reported beside it (kernel_ms_avg)
+        p_s = cnt.get("kernel_ms_rocprof", k_avg_s * 1e3) / 1e3
         roofline.update({
-            "achieved": round(f64 / k_avg_s / 1e12, 3), "frac": round(f64 / k_avg_s / 1e12 / FP64_PEAK_TFLOPS, 4),
-            "what": "executed fp64 flops (VALU FMA x2 + ADD/MUL + fp64 MFMA) per launch / launch time; FP64 pipe peak",
+            "achieved": round(f64 / p_s / 1e12, 3), "frac": round(f64 / p_s / 1e12 / FP64_PEAK_TFLOPS, 4),
+            "what": "executed fp64 flops (VALU FMA x2 + ADD/MUL + fp64 MFMA) per launch / the profiled launch's "
+                    "rocprof duration; FP64 pipe peak",
+            "kernel_ms_rocprof": round(p_s * 1e3, 3),
             "traffic": int(cnt["hbm_bytes"]),
             "traffic_note": "FETCH_SIZE x2 + WRITE_SIZE per launch (gfx950 correction), profile of this command",
-            "hbm": {"achieved_GBs": round(cnt["hbm_bytes"] / k_avg_s / 1e9, 1),
-                    "frac_of_8TBs": round(cnt["hbm_bytes"] / k_avg_s / 1e9 / HBM_PEAK_GBS, 4),
+            "hbm": {"achieved_GBs": round(cnt["hbm_bytes"] / p_s / 1e9, 1),
+                    "frac_of_8TBs": round(cnt["hbm_bytes"] / p_s / 1e9 / HBM_PEAK_GBS, 4),
                     "compulsory_bytes": int(cnt["compulsory_bytes"]),
                     "traffic_over_compulsory": round(cnt["hbm_bytes"] / cnt["compulsory_bytes"], 2)},
-            "int8_mfma": {"achieved_TOPS": round(cnt["i8_ops"] / k_avg_s / 1e12, 2),
-                          "frac_of_5POPS": round(cnt["i8_ops"] / k_avg_s / 1e12 / I8_PEAK_TOPS, 4)},
+            "int8_mfma": {"achieved_TOPS": round(cnt["i8_ops"] / p_s / 1e12, 2),
+                          "frac_of_5POPS": round(cnt["i8_ops"] / p_s / 1e12 / I8_PEAK_TOPS, 4)},
             "issue": cnt["issue"]})
+        if "code_object" in cnt:
+            roofline["code_object"] = {k: v for k, v in cnt["code_object"].items() if "klein" in k and "Lb0ELb1ELb0E" in k}
     roofline["hbm_algorithmic_note"] = (
         f"SURVEY 8d B_alg = {b_alg(d)} B/sample counts R once per sample, but R is shared by every "
         f"chain (read once per 256-sample block from L2), so B_alg x rate is not an HBM quantity")
@@ -361,6 +383,7 @@ def main():
         "parity_check": parity,
         "certificate_redos": {"verified_subpanels": redos, "per_proposal": redos / (args.steps * nc * T)},
         "autocorrelation": acf,
+        "covariance": covariance,
         "roofline": roofline,
         "gemm": gemm,
         "kernel_ms": {"klein": round(k_ms / max(k_n, 1), 3), "bz": round(g_ms / max(g_n, 1), 3),

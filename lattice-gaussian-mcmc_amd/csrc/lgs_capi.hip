@@ -333,6 +333,9 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
     a.R = c->R.as<double>();
     a.cert = c->CERT.as<double>();
     a.z1cap = c->z1cap;
+    // test hook: scale the certificate's cap on sum |z_j| (a cap below the actual sums
+    // forces every 32-row-panel sub-panel through the verification / replay path)
+    if (const char* s = getenv("LGS_TEST_Z1CAP_SCALE")) a.z1cap *= atof(s);
     a.z1max = (unsigned long long*)c->flags.as<unsigned int>() + 1;
     return a;
 }

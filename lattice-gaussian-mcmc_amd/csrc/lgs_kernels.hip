@@ -1419,7 +1419,10 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     __builtin_amdgcn_readfirstlane(
                         (int)((lds_cdptr)rec_lds)[(top - 1 - (p_hi - 32)) * kRecStride + kRecSpec]) == 1) {
                     double term[16];
-                    bool ok = true;
+                    // the bound dmu assumes sum_{j>i} |z_j| <= z1cap; with every z of the
+                    // sub-panel 0 that sum is the one at its start (else: the sequential
+                    // path, whose end-of-sub-panel check verifies)
+                    bool ok = cert_lds[0][threadIdx.x] <= a.z1cap;
 #pragma unroll
                     for (int s = 0; s < 16; ++s) {
                         const lds_cdptr rec = (lds_cdptr)rec_lds + (top - 1 - s - (p_hi - 32)) * kRecStride;

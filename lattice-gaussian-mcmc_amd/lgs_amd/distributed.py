@@ -53,13 +53,18 @@ def collective_active() -> bool:
 def init_process_group(backend: str, local_rank: int, world: int, rank: int = 0):
     """Initialise torch.distributed for this rank: "nccl" (= RCCL on ROCm) binds the
     communicator to cuda:local_rank; gloo on CPU.  Without a launcher's environment
-    (world 1) a local TCP store on 127.0.0.1 is used."""
+    a one-rank group gets a private TCP store on 127.0.0.1; several ranks need the
+    launcher's MASTER_ADDR / MASTER_PORT (a per-process random port would leave
+    every rank waiting at its own rendezvous)."""
     import torch
     import torch.distributed as dist
     kw = {}
     if "RANK" not in os.environ or "WORLD_SIZE" not in os.environ:
         kw = dict(rank=rank, world_size=world)
-    if "MASTER_ADDR" not in os.environ:
+    if "MASTER_ADDR" not in os.environ or "MASTER_PORT" not in os.environ:
+        if world > 1:
+            raise RuntimeError(f"world size {world} needs MASTER_ADDR and MASTER_PORT in the environment "
+                               "(e.g. python -m torch.distributed.run --master-addr 127.0.0.1 ...)")
         s = socket.socket()
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -172,16 +177,26 @@ class StreamingShard:
     autocovariance sums of two scalar functionals of the first ``lag_chains``
     chains' kept states -- the coefficient z_k = round(<binv_row, v>) and
     1e-6 ||v||^2 -- across blocks, and ``reduce`` combines everything over the
-    ranks with one all-reduce."""
+    ranks with one all-reduce.
+
+    ``gram_every`` = k > 0 (needs ``advance.gram(G, S)``, which ADDS sum z z^T and
+    sum z over the chains' current states to int64 G (d x d) / S (d)): after every
+    k-th block the states the chains hold at that block's end -- kept states,
+    thinned to one per chain per k blocks -- enter an exact second-moment sum, so
+    the job's empirical covariance (base.py:154-160) comes back from the same
+    single all-reduce (``covariance``)."""
 
     def __init__(self, advance: Callable, n_chains: int, d: int, *, binv_row, device, lag_chains: int = 1024,
-                 lags: int = 16, first_step: int = 1):
+                 lags: int = 16, first_step: int = 1, gram_every: int = 0):
         import torch
         self.t = torch
         self.advance = advance
         self.nc, self.d, self.dev = n_chains, d, device
         self.lag_chains = min(n_chains, lag_chains)
         self.lags = lags
+        if gram_every and not hasattr(advance, "gram"):
+            raise ValueError("gram_every needs an advance callable with a gram(G, S) method")
+        self.gram_every = int(gram_every)
         self.binv = torch.as_tensor(np.asarray(binv_row, dtype=np.float64)).to(device)
         self.next_step = first_step
         # the per-block lag-sum update is ~20 small kernels; on a GPU it is replayed
@@ -200,16 +215,25 @@ class StreamingShard:
         self.lag_z = LagSums(t, self.lag_chains, self.lags, t.int64, self.dev)
         self.lag_v = LagSums(t, self.lag_chains, self.lags, t.float64, self.dev)
         self.steps_done = 0
+        self.blocks = 0
+        if self.gram_every:
+            self.G = t.zeros((self.d, self.d), dtype=t.int64, device=self.dev)
+            self.S = t.zeros(self.d, dtype=t.int64, device=self.dev)
+            self.n_gram = 0
         self._graph = None  # captured against the previous sums' buffers
 
     def step(self, n_steps: int):
         v = self.advance(self.next_step, n_steps, self.acc, self.mom)
         self.next_step += n_steps
         self.steps_done += n_steps
+        self.blocks += 1
         if v is not None:
             self._lag_update(v)
             self.lag_z.update_host(self.lag_chains, n_steps)
             self.lag_v.update_host(self.lag_chains, n_steps)
+        if self.gram_every and self.blocks % self.gram_every == 0:
+            self.advance.gram(self.G, self.S)
+            self.n_gram += self.nc
 
     def _lag_device(self, v):
         vs = v[:self.lag_chains]
@@ -238,15 +262,31 @@ class StreamingShard:
             self._lag_device(v)
 
     def reduce(self, group=None) -> dict:
-        """One all-reduce of [accepts, moments, lag sums of both functionals]."""
+        """One all-reduce of [accepts, moments, lag sums of both functionals, and
+        (gram_every) the thinned states' sum z z^T, sum z and count]."""
+        t = self.t
         parts = [self.acc.sum().reshape(1), self.mom] + self.lag_z.parts() + self.lag_v.parts()
+        if self.gram_every:
+            parts += [self.G, self.S, t.tensor([self.n_gram], dtype=t.int64, device=self.S.device)]
         r = allreduce_parts(parts, group=group)
-        return {"accepts": r[0], "moments": r[1], "lag_z": r[2:6], "lag_v": r[6:10]}
+        out = {"accepts": r[0], "moments": r[1], "lag_z": r[2:6], "lag_v": r[6:10]}
+        if self.gram_every:
+            out["gram"] = r[10:13]
+        return out
 
     @staticmethod
     def acf(parts):
         S, N, S1, n = [x.cpu().numpy() for x in parts]
         return LagSums.acf(S.astype(np.float64), N, float(S1[0]), float(n[0]))
+
+    @staticmethod
+    def covariance(parts) -> np.ndarray:
+        """Unbiased covariance (np.cov convention) of the thinned states from the
+        exact reduced sums (G, S, n) of ``reduce()["gram"]``."""
+        G, S, n = [x.cpu().numpy() for x in parts]
+        n = int(n[0])
+        s = S.astype(np.float64)
+        return (G.astype(np.float64) - np.outer(s, s) / n) / (n - 1)
 
 
 def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device, *, flags: int = 0,
@@ -254,7 +294,15 @@ def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device,
     """StreamingShard's advance over the HIP C-ABI: chain state resident on the
     device (coordinate-major z), one lgs_imhk call per block; v of every kept state
     into a preallocated (n_chains, block_steps, d) buffer.  The state tensors are
-    exposed as ``advance.state``."""
+    exposed as ``advance.state``; ``advance.gram(G, S)`` adds sum z z^T / sum z of
+    the chains' current states (lgs_gram, exact int8-digit MFMA).
+
+    Streams: the library runs on a dedicated torch stream that waits (on the GPU,
+    no host synchronisation) for everything the caller enqueued on its current
+    stream before each call -- the lag-sum update still reading the reused v
+    buffer, the zeroed accumulators -- and the caller's stream waits for the
+    library's work after it (lgs_imhk itself ends with a synchronisation of its
+    stream, so that wait is free)."""
     import torch
     from . import _capi
     st = {"z": torch.zeros((d, n_chains), dtype=torch.int32, device=device),
@@ -263,16 +311,33 @@ def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device,
           "v": torch.empty((n_chains, block_steps, d), dtype=torch.float64, device=device)
           if want_v and block_steps else None}
     fl = flags | _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR
+    lib_stream = torch.cuda.Stream(device=device)
+    ctx.set_stream(lib_stream.cuda_stream)
+
+    def _enter():
+        lib_stream.wait_stream(torch.cuda.current_stream(device))
+
+    def _leave():
+        torch.cuda.current_stream(device).wait_stream(lib_stream)
 
     def advance(first_step, n_steps, acc, mom):
         v = st["v"]
         if want_v and (v is None or v.shape[1] != n_steps):
             v = st["v"] = torch.empty((n_chains, n_steps, d), dtype=torch.float64, device=device)
+        _enter()
         ctx.imhk(seed, first_chain, n_chains, first_step, n_steps, 1, st["z"], st["lw"], st["init"], acc,
                  v_samples=v if want_v else None, moments=mom, flags=fl)
+        _leave()
         return v if want_v else None
 
+    def gram(G, S):
+        _enter()
+        ctx.gram(st["z"], sum_out=S, gram_out=G, coord_major=True, flags=_capi.LGS_DEVICE_PTRS)
+        _leave()
+
     advance.state = st
+    advance.gram = gram
+    advance.stream = lib_stream
     return advance
 
 
@@ -365,6 +430,9 @@ def imhk_sharded(compute: Callable, n_chains: int, n_steps: int, *, rank: int, w
     import torch
     import torch.distributed as dist
 
+    if collective_active() and dist.get_world_size(group) != world:
+        raise ValueError(f"imhk_sharded: world={world} but the active process group has "
+                         f"{dist.get_world_size(group)} ranks")
     first, count = shard_range(n_chains, rank, world)
     r = compute(first_chain=first, n_chains=count, first_step=first_step, n_steps=n_steps)
     parts = [torch.tensor([r.accepts, r.kept], dtype=torch.int64),

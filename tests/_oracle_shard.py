@@ -47,5 +47,11 @@ def oracle_advance_factory(oracle, R, cp, B, sigma, seed, first_chain, n_chains,
         mom += torch.from_numpy(np.concatenate([kept.sum(0), (kept * kept).sum(0)]))
         return torch.from_numpy(tr.astype(np.float64) @ B.T)
 
+    def gram(G, S):  # the chains' current states (gpu_advance: lgs_gram of z_state)
+        z = torch.from_numpy(st["state"]["z"].astype(np.int64))
+        G += z.T @ z
+        S += z.sum(0)
+
     advance.state = st
+    advance.gram = gram
     return advance

@@ -112,15 +112,17 @@ def _stream_stats(D, oracle, factory, RcpB, rank, world, torch):
     first, count = D.shard_range(6, rank, world)
     adv = factory(oracle, R, cp, B, 165.7, 99, first, count, mode=oracle.IMHK_WANG_LING)
     binv = np.linalg.inv(B)[B.shape[0] - 1]
-    sh = D.StreamingShard(adv, count, B.shape[0], binv_row=binv, device="cpu", lag_chains=6, lags=5)
+    sh = D.StreamingShard(adv, count, B.shape[0], binv_row=binv, device="cpu", lag_chains=6, lags=5,
+                          gram_every=2)
     sh.step(3)  # warm-up block, then fresh statistics as the bench does
     sh.reduce()
     sh.reset_stats()
-    for _ in range(3):
+    for _ in range(4):
         sh.step(4)
     st = sh.reduce()
     return {"accepts": st["accepts"].tolist(), "moments": st["moments"].tolist(),
-            "lag_z": [x.tolist() for x in st["lag_z"]], "lag_v": [x.tolist() for x in st["lag_v"]]}
+            "lag_z": [x.tolist() for x in st["lag_z"]], "lag_v": [x.tolist() for x in st["lag_v"]],
+            "gram": [x.tolist() for x in st["gram"]], "cov": D.StreamingShard.covariance(st["gram"]).tolist()}
 
 
 @pytest.mark.timeout(300)
@@ -143,4 +145,41 @@ def test_streaming_shard_gloo_world2_matches_single_process(oracle):
         assert out[r]["lag_z"] == single["lag_z"]          # int64: exact
         np.testing.assert_allclose(np.array(out[r]["lag_v"][0]), np.array(single["lag_v"][0]), rtol=1e-13)
         assert out[r]["lag_v"][1] == single["lag_v"][1]
-    assert 0 < single["accepts"][0] < 6 * 12  # Wang-Ling: some rejections
+        assert out[r]["gram"] == single["gram"]            # int64 sum z z^T, sum z, count: exact
+    assert 0 < single["accepts"][0] < 6 * 16  # Wang-Ling: some rejections
+    # the thinned Gram = the chains' states after blocks 2 and 4 of the timed stretch
+    # (steps 11 and 19: a 3-step warm-up block, then blocks of 4), base.py:154-160
+    R, cp, B = g
+    tr = oracle.imhk(R, cp, B, 165.7, 6, 19, seed=99, first_step=1, mode=oracle.IMHK_WANG_LING,
+                     trace=True)["trace"]
+    kept = np.concatenate([tr[:, 10], tr[:, 18]]).astype(np.int64)
+    assert single["gram"][2] == [12]
+    assert single["gram"][0] == (kept.T @ kept).tolist()
+    np.testing.assert_allclose(np.array(single["cov"]), np.cov(kept.T.astype(float)), rtol=1e-12, atol=1e-12)
+
+
+def test_init_process_group_needs_launcher_env_for_several_ranks(monkeypatch):
+    """A random per-process port only serves a one-rank group; several ranks without
+    MASTER_ADDR / MASTER_PORT would each wait at their own rendezvous."""
+    from lgs_amd import distributed as D
+    for k in ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    with pytest.raises(RuntimeError, match="MASTER_ADDR"):
+        D.init_process_group("gloo", 0, 2, rank=0)
+
+
+def test_imhk_sharded_rejects_world_mismatch(monkeypatch):
+    """world must be the active group's size: a world=2 shard inside a one-rank group
+    (or the reverse) would all-reduce / gather over the wrong set of ranks."""
+    import torch.distributed as dist
+    from lgs_amd import distributed as D
+    for k in ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    D.init_process_group("gloo", 0, 1)
+    try:
+        def compute(**kw):
+            raise AssertionError("must not run")
+        with pytest.raises(ValueError, match="process group"):
+            D.imhk_sharded(compute, 4, 2, rank=0, world=2)
+    finally:
+        dist.destroy_process_group()

@@ -99,3 +99,42 @@ def test_speculative_small_kind_subpanels(capi, oracle, cfg, center_scale, wl):
         assert float(dif.max()) < 2e-5
     else:
         assert rel < 1e-10
+
+
+@pytest.mark.parametrize("scale", [1.0, 0.02])
+def test_low_z1_cap_forces_verification_not_speculation(capi, oracle, scale, monkeypatch):
+    """The certificate's bound dmu = Ca + Cb * cap holds only while the sample's
+    sum |z_j| stays below the context's cap (twice the largest sum of recent
+    launches).  A 64-sample launch first sets a cap from few samples; a cap scaled
+    far below every sum (LGS_TEST_Z1CAP_SCALE) makes every sub-panel exceed it: the
+    sequential sub-panels verify / replay in the reference's order and the
+    speculative (all-small-kind) sub-panels must not be kept on a bound that no
+    longer holds.  NTRU n = 128 (d = 256): half the coordinates are speculative
+    q-coordinates.  Output must equal the reference-order kernel's."""
+    import torch
+    from lgs_amd import lattices
+    if scale != 1.0:
+        monkeypatch.setenv("LGS_TEST_Z1CAP_SCALE", str(scale))
+    B = lattices.ntru_basis(128, 12289, 3)
+    R, cp = oracle.qr_prepare(B)
+    ctx = capi.Context(0)
+    ctx.set_basis(R, cp, B, 165.7)
+    d = B.shape[0]
+    f = capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR
+    z0 = torch.empty((d, 64), dtype=torch.int32, device="cuda")
+    ctx.klein(5, 0, 64, z0, None, None, f)  # the cap now comes from these 64 samples
+    n = 1 << 14
+    za = torch.empty((d, n), dtype=torch.int32, device="cuda")
+    zb = torch.empty_like(za)
+    la = torch.empty(n, dtype=torch.float64, device="cuda")
+    lb = torch.empty_like(la)
+    ctx.resolved(reset=True)
+    ctx.klein(6, 1 << 20, n, za, None, la, f)
+    redos = ctx.resolved()
+    ctx.klein(6, 1 << 20, n, zb, None, lb, f | capi.LGS_EXACT_ORDER)
+    torch.cuda.synchronize()
+    print(f"cap scale {scale}: {redos} verified sub-panels")
+    if scale != 1.0:
+        assert redos >= n // 64  # every wave verified (cap below every sum)
+    assert int((za != zb).any(dim=0).sum()) == 0
+    assert float(((la - lb).abs() / lb.abs().clamp_min(1.0)).max()) < 1e-10

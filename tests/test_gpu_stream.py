@@ -50,3 +50,46 @@ def test_lag_sums_graph_replay_equals_eager():
         assert np.array_equal(a, b)
     for a, b in zip(v_g, v_e):
         assert np.array_equal(a, b)
+
+
+def _gpu_shard(sync_each: bool, blocks: int = 4):
+    """StreamingShard driven through gpu_advance (lgs_imhk on the library's stream,
+    the lag-sum graph and the thinned Gram on the caller's), C2 q-ary d = 128."""
+    import torch
+    from lgs_amd import _capi
+    from lgs_amd import distributed as D
+    from lgs_amd.lattices import build_config
+    import lgs_oracle
+    lat, sigma = build_config("C2_qary128")
+    B = lat.basis
+    R, cp = lgs_oracle.qr_prepare(B)
+    d = B.shape[0]
+    ctx = _capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    dev = torch.device("cuda", 0)
+    nc, T = 2048, 16
+    adv = D.gpu_advance(ctx, 31, 0, nc, d, dev, flags=_capi.LGS_WANG_LING, block_steps=T)
+    sh = D.StreamingShard(adv, nc, d, binv_row=np.linalg.inv(B)[d - 1], device=dev, lag_chains=512, lags=6,
+                          gram_every=2)
+    for _ in range(blocks):
+        sh.step(T)
+        if sync_each:
+            torch.cuda.synchronize()
+    st = sh.reduce()
+    torch.cuda.synchronize()
+    return {k: ([x.cpu().numpy().copy() for x in v] if isinstance(v, list) else v.cpu().numpy().copy())
+            for k, v in st.items()}
+
+
+def test_gpu_advance_streams_match_synchronized_run():
+    """The library's stream waits for the caller's stream before each call (the lag
+    update still reading the reused v buffer): results equal a run synchronised
+    after every block."""
+    a = _gpu_shard(False)
+    b = _gpu_shard(True)
+    assert set(a) == set(b) and "gram" in a
+    for k in a:
+        xa, xb = (a[k], b[k]) if isinstance(a[k], list) else ([a[k]], [b[k]])
+        for x, y in zip(xa, xb):
+            assert np.array_equal(x, y), k
+    assert 0 < int(a["accepts"][0]) < 2048 * 64

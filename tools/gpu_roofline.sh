@@ -22,4 +22,5 @@ for P in "sq1:$P1" "sq2:$P2" "fetch:FETCH_SIZE" "write:WRITE_SIZE"; do
 done
 D=$(python3 -c "import sys; sys.path.insert(0,'lattice-gaussian-mcmc_amd'); from lgs_amd.lattices import build_config; print(build_config('$CFG')[0].basis.shape[0])")
 UNITS=$(python3 -c "import json; l=[x for x in open('$O/bench_trace.log') if x.startswith('{')][-1]; print(json.loads(l)['roofline']['units_per_launch'])")
-python3 tools/roofline_counters.py $O $CFG $UNITS $D $O/${TAG}_klein_counters.json $O/bench_trace.log
+python3 tools/co_resources.py --filter _ZN3lgs --json $O/${TAG}_co_resources.json > $O/co_resources.txt
+python3 tools/roofline_counters.py $O $CFG $UNITS $D $O/${TAG}_klein_counters.json $O/bench_trace.log $O/${TAG}_co_resources.json

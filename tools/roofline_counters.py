@@ -2,6 +2,7 @@
 bench.py's roofline (tools/gpu_roofline.sh).
 
 usage: roofline_counters.py <profile dir> <config> <units_per_launch> <d> <out.json> [bench_trace.log]
+                            [co_resources.json]
 
 The build id of the library the profiled bench loaded (its JSON line's
 roofline.build_id, from the optional log) is stored with the counters: bench.py
@@ -53,6 +54,20 @@ res = {"config": config, "units_per_launch": units, "grid_size": grid_max, "buil
        "i8_ops": 32768 * max(avg.get("SQ_INSTS_MFMA", 0) - f64_mfma, 0),
        "hbm_bytes": 1024 * (2 * avg.get("FETCH_SIZE", 0) + avg.get("WRITE_SIZE", 0)),
        "compulsory_bytes": units * d * 2 + 8 * d * (d + 1) // 2}
+# the profiled run's own duration of those launches (kernel trace of the same
+# command): bench.py divides the counters by THIS time, so every fraction is of one
+# run; its HIP-event time of the timed run is reported beside it
+durs = []
+for f in glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "klein_mfma_kernel" not in r.get("Kernel_Name", ""):
+            continue
+        g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        if g == grid_max:
+            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+if durs:
+    res["kernel_ms_rocprof"] = sum(durs) / len(durs)
+    res["kernel_launches_rocprof"] = len(durs)
 wc = avg.get("SQ_WAVE_CYCLES")
 if wc:
     res["issue"] = {"valu_active_per_wave_cycle": round(avg.get("SQ_ACTIVE_INST_VALU", 0) / wc, 4),
@@ -60,5 +75,13 @@ if wc:
                     "waiting_on_memory_or_barrier": round(avg.get("SQ_WAIT_ANY", 0) / wc, 4),
                     "waiting_on_issue": round(avg.get("SQ_WAIT_INST_ANY", 0) / wc, 4),
                     "valu_insts_per_wave": round(avg.get("SQ_INSTS_VALU", 0) / (waves or 1), 1)}
+if len(sys.argv) > 7 and os.path.exists(sys.argv[7]):  # code-object resources of the profiled build
+    co = json.load(open(sys.argv[7]))
+    res["code_object"] = {k["name"]: {f: k.get(f) for f in ("vgpr_count", "agpr_count", "sgpr_count",
+                                                               "vgpr_spill_count", "sgpr_spill_count",
+                                                               "private_segment_fixed_size",
+                                                               "group_segment_fixed_size", "waves_per_simd")}
+                          for k in co["kernels"] if "klein_mfma_kernel" in k["name"] or "bz_i8" in k["name"]}
+    res["code_object_build_id"] = co.get("build_id")
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: v for k, v in res.items() if k != "counters_per_launch"}))
