@@ -98,6 +98,14 @@ struct lgs_ctx {
     DevBuf CREC, RX;              // 32-row panels: per-coordinate records, coupling blocks
     DevBuf CERT;                  // per coordinate {Ca, Cb}: decision certificate
     uint64_t n_resolved = 0;      // sub-panel verifications of uncertified decisions
+    // certified Wang-Ling accept decisions (imhk_accept_cert_kernel): R transposed,
+    // the per-proposal weight bounds, the running maximum bound (device word, reset
+    // by lgs_set_basis), counters of resolved decisions and of recomputed draws that
+    // did not reproduce the stored z (0 unless a bug)
+    DevBuf RT, LWE, EMAX;
+    DevBuf QZ2;            // per 32-row panel: the q-panel skip's bound on ||z_W||^2 (klein_mfma_kernel)
+    bool has_qz2 = false;
+    uint64_t n_accept_resolved = 0, n_wl_mismatch = 0;
     uint64_t n_fallback = 0;      // Klein launches redone with a wider store / fp64 far field
     // 32-row-panel kernels: the certificate's bound on sum_j |z_j| of a sample (an
     // estimate from the basis, then twice the largest sum seen; a sample exceeding it
@@ -108,11 +116,14 @@ struct lgs_ctx {
     bool has_rd = false, oz_off = false;  // oz_off: a |z| > 32767 was seen (sticky)
     DevBuf H16, F0;               // int8-digit far field scratch: coefficient history, tile-0 sums
     DevBuf ZNZ;                   // per history block and lane: any nonzero z (B z's chunk skipping)
+    DevBuf CLIVE;                 // per wave and 64-coordinate chunk: any nonzero z (bits; B z)
     // the last Klein launch's history, valid for columns [0, cols) of the store Z it
     // wrote (B z reads its digits from there); reset by every Klein launch
     struct {
         const void* Z = nullptr;
         int64_t lanes = 0, cols = 0;
+        const unsigned int* clive = nullptr;  // its per-wave chunk bits (nullable)
+        int64_t clive_ld = 0;
     } hist;
     DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
     DevBuf kchunk, koff;          // per 128-row tile of B: the 64-column chunks with a non-zero digit
@@ -258,8 +269,10 @@ int finish(lgs_ctx* c, const unsigned int* fw_known = nullptr) {  // sync, fold 
     c->resolved_seen = 0;
     if (fw[1] || fw[2] || fw[3])
         fold_counters(c, fw);
-    if (fw[1] || fw[2] || fw[3] || fw[4] || fw[5])  // ordered before the next launches on the stream
-        HIP_TRY(hipMemsetAsync((unsigned int*)c->flags.p + 1, 0, 5 * sizeof(unsigned int), c->stream));
+    c->n_accept_resolved += fw[lgs::kFlagWordAcceptResolved];
+    c->n_wl_mismatch += fw[lgs::kFlagWordWLMismatch];
+    if (fw[1] || fw[2] || fw[3] || fw[4] || fw[5] || fw[6] || fw[7])  // ordered before the next launches
+        HIP_TRY(hipMemsetAsync((unsigned int*)c->flags.p + 1, 0, 7 * sizeof(unsigned int), c->stream));
     if (f & lgs::kFlagNonFinite)
         return fail(LGS_ERR_NONFINITE, "non-finite conditional mean (reference raises ValueError)");
     if (f & lgs::kFlagOverflow)
@@ -337,6 +350,8 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
     // forces every 32-row-panel sub-panel through the verification / replay path)
     if (const char* s = getenv("LGS_TEST_Z1CAP_SCALE")) a.z1cap *= atof(s);
     a.z1max = (unsigned long long*)c->flags.as<unsigned int>() + 1;
+    const bool no_qskip = getenv("LGS_NO_QSKIP") && atoi(getenv("LGS_NO_QSKIP")) == 1;  // A/B switch
+    a.qz2 = c->has_qz2 && !no_qskip ? c->QZ2.as<double>() : nullptr;
     return a;
 }
 
@@ -367,6 +382,15 @@ int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int zb, void* 
         if (rc) return rc;
         if ((rc = c->ZNZ.reserve((size_t)blocks * lanes))) return rc;
         a.znz = c->ZNZ.as<uint8_t>();
+#ifndef LGS_NEAR_UNROLLED
+        if (c->d % 16 == 0) {  // per-wave chunk bits for B z (zeroed: the kernel ORs into them)
+            const int64_t words = (c->d + 2047) / 2048 * (lanes / 64);
+            if ((rc = c->CLIVE.reserve((size_t)words * 4))) return rc;
+            HIP_TRY(hipMemsetAsync(c->CLIVE.p, 0, (size_t)words * 4, c->stream));
+            a.clive = c->CLIVE.as<unsigned int>();
+            a.clive_ld = lanes / 64;
+        }
+#endif
         a.rd = c->RD.as<int8_t>();
         a.rd_off = c->RDOFF.as<int64_t>();
         a.h16 = c->H16.as<int16_t>();
@@ -393,6 +417,8 @@ int run_klein_store(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int& zb,
         c->hist.Z = Z;
         c->hist.lanes = (a.n + 63) / 64 * 64;
         c->hist.cols = a.n;
+        c->hist.clive = a.clive;
+        c->hist.clive_ld = a.clive_ld;
     }
     if (rc || deferred || (zb != 2 && !oz)) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -451,7 +477,8 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
                                (int)c->bd_cols, (int)c->d, n, V, c->d, b.rb,
                                b.rstride, b.roff, c->flags.as<unsigned int>(),
                                after_klein && c->hist.Z == Z && Z ? c->H16.as<int16_t>() : nullptr, c->hist.lanes,
-                               c->hist.cols, c->stream, abort, c->ZNZ.as<uint8_t>()));
+                               c->hist.cols, c->stream, abort, c->ZNZ.as<uint8_t>(),
+                               after_klein && c->hist.Z == Z && Z ? c->hist.clive : nullptr, c->hist.clive_ld));
     c->pending_i8.push_back(b);
     return LGS_OK;
 }
@@ -761,6 +788,51 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
         }
         for (int64_t i = top - 16; i < top; ++i) crec[i * lgs::kRecStride + lgs::kRecSpec] = all ? 1.0 : 0.0;
     }
+    // q-panel skip (klein_mfma_kernel, reference mode): for a 32-row panel whose rows
+    // all lie in speculative sub-panels, the largest ||z_W||_2^2 (W = coordinates
+    // outside speculative sub-panels; the kernel tracks it per sample while every
+    // speculative z so far is 0) for which every row i is certified z_i = 0 without
+    // its mean: the reference's mean obeys
+    //   |mu_i| <= (|c'_i| + (1 + g) sum_j |R_ij z_j|) (1 + 3u) / R_ii,
+    //   sum_j |R_ij z_j| <= G_i ||z_W||,  G_i = ||R[i, j > i, j in W]||_2  (Cauchy-Schwarz),
+    // g = 1.1 d u (the sum's rounding), and the one-dominant-point decision z = rint(mu)
+    // = 0 holds for every |mu| < theta_i = 1/2 - 745.2 / (is_i^2 (1 - 1e-12)) (all other
+    // window points below e^-745.2, lgs_device.h; q[7] == 0: the window ends carry 0).
+    std::vector<double> qz2((size_t)npan32, -1.0);
+    bool any_q = false;
+    if (!(flags & LGS_BASIS_LINEAR_PROBS)) {
+        std::vector<char> inW(dd);
+        for (size_t i = 0; i < dd; ++i) inW[i] = crec[i * lgs::kRecStride + lgs::kRecSpec] == 0.0;
+        const double g = 1.1 * (double)d * std::ldexp(1.0, -53);
+        for (int64_t pk = 0; pk < npan32; ++pk) {
+            const int64_t p_hi = d - 32 * pk;
+            if (p_hi < 32) break;
+            bool all = true;
+            for (int64_t i = p_hi - 32; i < p_hi && all; ++i) all = !inW[i];
+            if (!all) continue;
+            double zmin = INFINITY;
+            for (int64_t i = p_hi - 32; i < p_hi; ++i) {
+                long double g2 = 0.0L;
+                for (int64_t j = i + 1; j < d; ++j)
+                    if (inW[j]) g2 += (long double)R[i * dd + j] * (long double)R[i * dd + j];
+                const double Gi = (double)sqrtl(g2) * (1.0 + 1e-13);
+                const double is = szc[i * lgs::kSzcStride + 1];
+                const double theta = 0.5 - 745.2 / (is * is * (1.0 - 1e-12)) - 1e-9;
+                const double num = theta * co[dd + i] * (1.0 - 1e-12) - std::fabs(co[i]);
+                const double zi = num <= 0.0 ? -1.0 : (Gi > 0.0 ? num / ((1.0 + g) * Gi) : INFINITY);
+                zmin = std::min(zmin, zi);
+            }
+            if (zmin > 0.0) {
+                qz2[pk] = std::isinf(zmin) ? INFINITY : zmin * zmin * (1.0 - 1e-12);
+                any_q = true;
+            }
+        }
+    }
+    c->has_qz2 = any_q;
+    if (any_q) {
+        if ((rc = c->QZ2.reserve(qz2.size() * 8))) return rc;
+        HIP_TRY(hipMemcpy(c->QZ2.p, qz2.data(), qz2.size() * 8, hipMemcpyHostToDevice));
+    }
     c->has_rd = oz;
     if (oz) {
         if ((rc = c->RD.reserve(rdv.size())) || (rc = c->RDOFF.reserve(rdoff.size() * 8))) return rc;
@@ -780,6 +852,14 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     HIP_TRY(hipMemcpy(c->RP.p, rp.data(), rp.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->RC.p, rcv.data(), rcv.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->coord.p, co.data(), co.size() * 8, hipMemcpyHostToDevice));
+    {  // R transposed (certified Wang-Ling accept decisions: reference-order means, coalesced)
+        std::vector<double> rt(dd * dd);
+        for (size_t r = 0; r < dd; ++r)
+            for (size_t k = 0; k < dd; ++k) rt[k * dd + r] = R[r * dd + k];
+        if ((rc = c->RT.reserve(dd * dd * 8)) || (rc = c->EMAX.reserve(8))) return rc;
+        HIP_TRY(hipMemcpy(c->RT.p, rt.data(), dd * dd * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemset(c->EMAX.p, 0, 8));
+    }
     c->has_B = B != nullptr;
     if (B) {
         std::vector<double> bt(dd * dd);
@@ -848,7 +928,7 @@ int lgs_klein(lgs_ctx* c, uint64_t seed, uint64_t first, int64_t n, void* z_out,
     if (n == 0) return LGS_OK;
     const bool dev = flags & LGS_DEVICE_PTRS, z64 = flags & LGS_Z64,
                cm = flags & LGS_COORD_MAJOR, exact = flags & LGS_EXACT_ORDER,
-               wl = flags & LGS_WANG_LING;
+               wl = flags & LGS_WANG_LING, bound = flags & LGS_LOGW_BOUND;
     if (v_out && !c->has_B) return fail(LGS_ERR_STATE, "v_out requires B");
     const int64_t d = c->d;
     const int ob = z64 ? 8 : 4;  // caller's coefficient width
@@ -879,6 +959,15 @@ int lgs_klein(lgs_ctx* c, uint64_t seed, uint64_t first, int64_t n, void* z_out,
             a.ldz = m;
         }
         a.LW = logw_out ? (dev ? logw_out + off : c->LW.as<double>()) : nullptr;
+        if (wl && !exact) a.emax = c->EMAX.as<unsigned long long>();
+        if (wl && bound && logw_out) {  // the weights' bounds into logw_out[n .. 2n)
+            if (dev) {
+                a.LWE = logw_out + n + off;
+            } else {
+                if ((rc = c->LWE.reserve((size_t)chunk * 8))) return rc;
+                a.LWE = c->LWE.as<double>();
+            }
+        }
         if ((rc = run_klein_store(c, a, exact, wl, zb, Zp, false))) return rc;
         if (z_out && !direct) {
             if (cm) {  // coordinate-major output through host pointers (zb == ob)
@@ -904,6 +993,9 @@ int lgs_klein(lgs_ctx* c, uint64_t seed, uint64_t first, int64_t n, void* z_out,
         }
         if (logw_out && !dev)
             HIP_TRY(hipMemcpyAsync(logw_out + off, a.LW, (size_t)m * 8, hipMemcpyDeviceToHost,
+                                   c->stream));
+        if (logw_out && !dev && a.LWE)
+            HIP_TRY(hipMemcpyAsync(logw_out + n + off, a.LWE, (size_t)m * 8, hipMemcpyDeviceToHost,
                                    c->stream));
         if (!dev || v_out) {  // staging buffers / the int8-digit replay need the chunk intact
             if ((rc = finish(c))) return rc;
@@ -1020,6 +1112,9 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
     int zb = z64 ? 8 : c->zint;      // internal proposal store width
     const int64_t n_keep = n_steps / thin;
     if ((rc = reset_flags(c))) return rc;
+    // Wang-Ling weights of the blocked kernels carry a bounded error: certify each
+    // accept decision against it (LGS_EXACT_ORDER weights are the reference's)
+    const bool certw = wl && !exact;
 
     // ---- block of T steps (a multiple of thin) per Klein launch
     int64_t T = std::max<int64_t>(1, c->max_props / nc);
@@ -1034,7 +1129,7 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
         (rc = c->LW.reserve((size_t)np * 8)) ||
         (rc = c->sel.reserve((size_t)std::max<int64_t>(nc * kmax, nc) * 8)) ||
         (rc = c->fsel.reserve((size_t)nc * 8)) || (rc = c->cnt.reserve((size_t)np * 4)) ||
-        (rc = c->ccnt.reserve((size_t)nc * 4)))
+        (rc = c->ccnt.reserve((size_t)nc * 4)) || (certw && (rc = c->LWE.reserve((size_t)np * 8))))
         return rc;
 
     // ---- device views of the chain state (staged through device buffers for host pointers)
@@ -1096,6 +1191,7 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
             a.n = nc;
             a.ldz = nc;
             a.LW = c->LW.as<double>();
+            if (certw) a.emax = c->EMAX.as<unsigned long long>();  // (the initial states' bound)
             a.gate = fl + kFlagWordUninit;
             bool oz0 = false;
             if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p, true, &oz0))) return rc;
@@ -1122,6 +1218,10 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
         a.n = npb;
         a.ldz = ldzb;
         a.LW = c->LW.as<double>();
+        if (certw) {
+            a.LWE = c->LWE.as<double>();
+            a.emax = c->EMAX.as<unsigned long long>();
+        }
         bool ozb = false;
         if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p, true, &ozb))) return rc;
         oz_used |= ozb;
@@ -1150,9 +1250,25 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
         aa.acc_step = accs ? accs + t0 : nullptr;
         aa.acc_ld = n_steps;
         aa.abort = fl;
+        if (certw) {  // certified Wang-Ling decisions (imhk_accept_cert_kernel)
+            aa.LWE = c->LWE.as<double>();
+            aa.emax = c->EMAX.as<unsigned long long>();
+            aa.LWx = c->LW.as<double>();
+            aa.RT = c->RT.as<double>();
+            aa.Zst = c->Z.p;
+            aa.zb = zb;
+            aa.ldz = ldzb;
+            aa.zs = zs;
+            aa.ob = ob;
+            aa.zs_cm = cm ? 1 : 0;
+            aa.flagw = fl;
+            // test hook: widened bounds force the recomputation path on many decisions
+            const char* bs = getenv("LGS_TEST_WL_BOUND_SCALE");
+            aa.bscale = bs ? atof(bs) : 1.0;
+        }
         {
             Scope s(c, 2);
-            HIP_TRY(lgs::launch::accept(aa, c->stream));
+            HIP_TRY(lgs::launch::accept(aa, a, c->stream));
         }
         // The final-state gather rides on the moments pass unless a later step of this
         // block still reads the carried-in states (kept-state gather without carry columns).
@@ -1272,9 +1388,12 @@ int lgs_timing_get(lgs_ctx* c, int kernel, double* ms, int64_t* n) {
 
 int lgs_counter(lgs_ctx* c, int which, int reset, uint64_t* value) {
     if (!c) return fail(LGS_ERR_INVALID, "null context");
-    if (which != LGS_COUNTER_RESOLVED && which != LGS_COUNTER_FALLBACK)
-        return fail(LGS_ERR_INVALID, "counter id 0..1");
-    uint64_t& v = which == LGS_COUNTER_RESOLVED ? c->n_resolved : c->n_fallback;
+    if (which < LGS_COUNTER_RESOLVED || which > LGS_COUNTER_WL_MISMATCH)
+        return fail(LGS_ERR_INVALID, "counter id 0..3");
+    uint64_t& v = which == LGS_COUNTER_RESOLVED      ? c->n_resolved
+                  : which == LGS_COUNTER_FALLBACK    ? c->n_fallback
+                  : which == LGS_COUNTER_ACCEPT_RESOLVED ? c->n_accept_resolved
+                                                     : c->n_wl_mismatch;
     if (value) *value = v;
     if (reset) v = 0;
     return LGS_OK;
@@ -1445,18 +1564,18 @@ int lgs_gram(lgs_ctx* c, int64_t d, int64_t n, const void* x, int64_t ldx, const
         int8_t* Pl = Ph + (size_t)dpad * ldp;
         unsigned int f = 0;
         {
+            // the planes pass is gated on the packing's range flag on the device, so both
+            // are enqueued before the one synchronisation
             Scope s(c, 4);
             HIP_TRY(lgs::launch::gram_pack(Xin, xt, cm, ldx, (int)d, n, (const long long*)SH, Ph, Pl, ldp,
                                            c->flags.as<unsigned int>(), c->stream));
+            HIP_TRY(lgs::launch::gram_planes(Ph, Pl, ldp, (int)d, G, S, c->stream, c->flags.as<unsigned int>()));
         }
         HIP_TRY(hipMemcpyAsync(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         if (f & lgs::kFlagI8Range) {
-            valu = true;  // some |x - shift| > 32639: exact int64 VALU
+            valu = true;  // some |x - shift| > 32639: exact int64 VALU (the planes pass returned at once)
             HIP_TRY(hipMemsetAsync(c->flags.p, 0, 16, c->stream));
-        } else {
-            Scope s(c, 4);
-            HIP_TRY(lgs::launch::gram_planes(Ph, Pl, ldp, (int)d, G, S, c->stream));
         }
     }
     if (valu) {

@@ -267,7 +267,11 @@ __global__ __launch_bounds__(512) void gram_planes_kernel(const int8_t* __restri
                                                           const int8_t* __restrict__ Pl, int64_t ldp,
                                                           int d, int64_t np, int64_t kc, int nt,
                                                           unsigned long long* __restrict__ G,
-                                                          unsigned long long* __restrict__ S) {
+                                                          unsigned long long* __restrict__ S,
+                                                          const unsigned int* gate) {
+    // gate (nullable): the packing found a |y| beyond two digits -- the exact VALU
+    // replay runs instead (decided on the device: no host round trip between the passes)
+    if (gate && (*(const volatile unsigned int*)gate & kFlagI8Range)) return;
     constexpr int BT = 128, KC = 64, P = 80;
     __shared__ __attribute__((aligned(16))) int8_t A1[BT * P], A0[BT * P], B1[BT * P], B0[BT * P];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -355,7 +359,9 @@ __global__ __launch_bounds__(512) void gram_planes_kernel(const int8_t* __restri
 }
 
 // lower block triangle := upper (tiles ti < tj of 128); diagonal tiles are full
-__global__ __launch_bounds__(256) void gram_mirror_kernel(unsigned long long* __restrict__ G, int d) {
+__global__ __launch_bounds__(256) void gram_mirror_kernel(unsigned long long* __restrict__ G, int d,
+                                                          const unsigned int* gate) {
+    if (gate && (*(const volatile unsigned int*)gate & kFlagI8Range)) return;
     const int j = blockIdx.x * 16 + (threadIdx.x & 15);   // column of the lower entry
     const int i = blockIdx.y * 16 + (threadIdx.x >> 4);   // row
     if (i >= d || j >= d || (i >> 7) <= (j >> 7)) return;
@@ -716,7 +722,7 @@ hipError_t gram_pack(const void* X, int xtype, bool coord_major, int64_t ldx, in
 }
 
 hipError_t gram_planes(const int8_t* Ph, const int8_t* Pl, int64_t ldp, int d, void* G, void* S,
-                       hipStream_t st) {
+                       hipStream_t st, const unsigned int* gate) {
     const int nt = (d + 127) / 128;
     const int64_t pairs = (int64_t)nt * (nt + 1) / 2;
     // about 2 workgroups (16 waves) per CU, K chunks of 64..16384 samples
@@ -727,10 +733,10 @@ hipError_t gram_planes(const int8_t* Ph, const int8_t* Pl, int64_t ldp, int d, v
     if (kc < 64) kc = 64;
     const dim3 grid((unsigned)pairs, (unsigned)((ldp + kc - 1) / kc));
     hipLaunchKernelGGL(gram_planes_kernel, grid, dim3(512), 0, st, Ph, Pl, ldp, d, ldp, kc, nt,
-                       (unsigned long long*)G, (unsigned long long*)S);
+                       (unsigned long long*)G, (unsigned long long*)S, gate);
     if (nt > 1)
         hipLaunchKernelGGL(gram_mirror_kernel, dim3((unsigned)((d + 15) / 16), (unsigned)((d + 15) / 16)),
-                           dim3(256), 0, st, (unsigned long long*)G, d);
+                           dim3(256), 0, st, (unsigned long long*)G, d, gate);
     return hipGetLastError();
 }
 

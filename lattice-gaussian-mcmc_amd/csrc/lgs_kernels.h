@@ -131,7 +131,26 @@ struct KleinArgs {
     const double* rx;    // per 32-row panel: 16x16 block R[p_hi-32.., p_hi-16..] as MFMA A fragments
     const unsigned int* gate;  // nullable: when *gate == 0 every block returns at once (initial draws
                                // of lgs_imhk when no chain needs one, decided on the device)
+    // Wang-Ling mode, blocked kernels (nullable): per sample a bound E >= |LW - LW_ref|,
+    // LW_ref = the log weight at the reference-order means (what klein_exact_kernel
+    // returns), from the certificate's bound on each mean (lgs_kernels.hip wl_bound_*)
+    double* LWE;
+    unsigned long long* emax;  // nullable: atomicMax of those bounds (fp64 bits, E >= 0)
+    // q-panel skip (reference mode, int8-digit far field; nullable): per 32-row panel the
+    // largest ||z_W||^2 for which every row's mean is certified to give z = 0 without
+    // computing it (lgs_set_basis), < 0 where it does not apply
+    const double* qz2;
+    // nullable (with h16, d % 16 == 0): per wave of the launch, bit c & 31 of word
+    // clive[(c >> 5) * clive_ld + wave] set when some lane has a nonzero z in the
+    // 64-coordinate chunk c (zeroed before the launch; B z's chunk skipping)
+    unsigned int* clive;
+    int64_t clive_ld;
 };
+
+// Counter / check words of the context's flag buffer used by the certified
+// Wang-Ling accept decisions (imhk_accept_kernel)
+constexpr int kFlagWordAcceptResolved = 6;  // decisions redone at reference-order weights
+constexpr int kFlagWordWLMismatch = 7;      // recomputed draws that did not reproduce the stored z (a bug)
 
 struct AcceptArgs {
     int64_t nc;
@@ -154,6 +173,23 @@ struct AcceptArgs {
     uint8_t* acc_step;   // nullable: 1 where step t of chain c accepted, at acc_step[c * acc_ld + t]
     int64_t acc_ld;
     const unsigned int* abort;  // nullable: return at once when *abort & kAbortMask
+    // Certified Wang-Ling decisions (LWE non-null, blocked kernels): each decision is
+    // taken only when it is the same for every pair of weights within the bounds
+    // LWE (proposals) / *emax (chain states carried into the block) of the stored
+    // ones; otherwise both weights are recomputed in the reference's order by the
+    // wave (wl_exact_wave) and written back with bound 0.
+    double* LWE;
+    const unsigned long long* emax;
+    double* LWx;            // = LW, writable (recomputed weights)
+    const double* RT;       // R transposed, d x d (RT[j * d + i] = R[i][j])
+    const void* Zst;        // proposal store (coordinate-major, column p, ld ldz, zb-byte elements)
+    int zb;
+    int64_t ldz;
+    const void* zs;         // chain states carried into the block (caller's layout)
+    int ob;
+    int zs_cm;
+    unsigned int* flagw;    // the context's flag words (kFlagWordAcceptResolved, kFlagWordWLMismatch)
+    double bscale;          // bounds x bscale (1; a test hook widens them to force recomputations)
 };
 
 // Per-series statistics (lgs_diag.hip series_stats_kernel).  Series s starts at
@@ -191,7 +227,7 @@ hipError_t gram_pack(const void* X, int xtype, bool coord_major, int64_t ldx, in
                      const long long* shift, int8_t* Ph, int8_t* Pl, int64_t ldp, unsigned int* flags,
                      hipStream_t st);
 hipError_t gram_planes(const int8_t* Ph, const int8_t* Pl, int64_t ldp, int d, void* G, void* S,
-                       hipStream_t st);
+                       hipStream_t st, const unsigned int* gate = nullptr);
 hipError_t jump(const void* x, int xtype, int64_t n, int d, int64_t ld, double* out, hipStream_t st);
 hipError_t tvd_minmax(const void* x, int xtype, int64_t n, int d, long long* mn, long long* mx,
                       unsigned int* flags, hipStream_t st);
@@ -212,7 +248,8 @@ hipError_t hist_counts(const void* x, int xtype, int64_t n, int d, int64_t nb, c
 // zb / ob / ib: coefficient element width in bytes (2, 4 or 8)
 hipError_t klein(const KleinArgs& a, const double* R, const double* RP, const double* RC,
                  int panel, int kernel, bool wl, int zb, void* Z, hipStream_t st);
-hipError_t accept(const AcceptArgs& a, hipStream_t st);
+// ka: the launch's Klein arguments (certified Wang-Ling decisions recompute weights)
+hipError_t accept(const AcceptArgs& a, const KleinArgs& ka, hipStream_t st);
 hipError_t samplez_probe(const double* mu, const double* sig, const double* u, int64_t n,
                          int precision, int linear, int mode, const double* etab, int64_t* z, double* ln,
                          hipStream_t st);
@@ -250,7 +287,8 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
-                 hipStream_t st, const unsigned int* abort = nullptr, const uint8_t* znz = nullptr);
+                 hipStream_t st, const unsigned int* abort = nullptr, const uint8_t* znz = nullptr,
+                 const unsigned int* clive = nullptr, int64_t clive_ld = 0);
 // ---- decoding
 // V (row-major n x d) = rows s: sum_c MT[c][r] X[c][s], X coordinate-major fp64 (fp64 MFMA)
 hipError_t gemm_f64(const double* X, int64_t ldx, const double* MT, int d, int64_t n, double* V,

@@ -64,13 +64,44 @@ __device__ __forceinline__ double cert_dmu(double ca, double cb, double z1, doub
     return fma(cb, z1, ca) + 6e-16 * fabs(mu);
 }
 
+// Wang-Ling weight bounds (certified decisions, blocked kernels).  A coordinate's
+// term is the window's log normaliser ln(mu) = log sum_k exp(-(k - mu)^2 / (2 s^2))
+// (imhk.py:102-124 via the SampleZ table of klein.py:129-139), evaluated at the
+// blocked-order mean; the reference evaluates it at mu_ref, |mu - mu_ref| <= dmu
+// (the certificate).  d ln / d mu = E_w[k - mu] / s^2, so with every window point
+// within hw of mu:  |ln(mu) - ln(mu_ref)| <= (hw + dmu) dmu / s^2.  The window is
+// the same at both means (certified decisions check its ends), and 1e-12 (1 + |ln|)
+// covers the two evaluations' rounding and the rare table-walk path (its sum of
+// <= 1001 terms against the closed / fitted normaliser).  One dominant point c
+// (ln = -(c - mu)^2 / (2 s^2), the same c at both means): the exact difference
+// (d1 + dmu / 2) dmu / s^2, d1 = |c - mu|, plus 1e-15 (1 + |ln|) for the three
+// roundings.  The sum over coordinates (same order in both kernels) adds at most
+// 2.5 u (d + 1) sum |terms| (wl_bound_sum).
+__device__ __forceinline__ double wl_bound_generic(double ln, double is, double hw, double dmu) {
+    return (hw + dmu) * (is * is) * dmu + 1e-12 * (1.0 + fabs(ln));
+}
+__device__ __forceinline__ double wl_bound_dominant(double emax, double is2, double d1, double dmu) {
+    return is2 * dmu * (d1 + 0.5 * dmu) + 1e-15 * (1.0 + fabs(emax));
+}
+__device__ __forceinline__ double wl_bound_sum(double eb, double tb, int d) {
+    return eb + 2.8e-16 * (double)(d + 1) * tb;
+}
+// half-width + 1 of the support window (klein.py:113-128): rf sigma, capped at 500
+__device__ __forceinline__ double wl_window_hw(double rf_sigma) { return fmin(rf_sigma, 500.0) + 1.0; }
+// per-sample bound out, and the wave's largest one into the context's running maximum
+__device__ __forceinline__ void wl_bound_store(const KleinArgs& a, int64_t p, double e) {
+    if (a.LWE) a.LWE[p] = e;
+    if (a.emax) atomicMax(a.emax, (unsigned long long)__double_as_longlong(e));
+}
+
 // One coordinate's decision + weight bookkeeping, shared by both samplers.
 // dmu >= 0: certified decision (kAmbiguous when the reference-order mean could
 // decide otherwise; lw is then untouched); dmu < 0: decide at mu.
+// WL: eb / tb accumulate the term's bound (wl_bound_generic) and |term|.
 template <bool WL, typename TP>
 __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double mu,
                                                CoordStream& rs, double& lw, unsigned int& flags,
-                                               TP etab, double dmu) {
+                                               TP etab, double dmu, double& eb, double& tb) {
     double zi;
     if (!isfinite(mu)) {
         flags |= kFlagNonFinite;
@@ -95,13 +126,24 @@ __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double
         zi = sample_z_coord(mu, rs.u((uint32_t)(a.d - 1 - i)), cst(a.szc) + (size_t)i * kSzcStride,
                             a.precision, a.linear_probs != 0, WL, etab, ln, dmu);
         if (zi == kAmbiguous) return kAmbiguous;
-        if (WL) lw += ln;
+        if (WL) {
+            lw += ln;
+            tb += fabs(ln);
+            if (dmu >= 0.0)
+                eb += wl_bound_generic(ln, cst(a.szc)[(size_t)i * kSzcStride + 1],
+                                       wl_window_hw(cst(a.szc)[(size_t)i * kSzcStride + 6]), dmu);
+        }
     } else {
         SampleZOut o = sample_z(mu, s, a.precision, a.linear_probs != 0,
                                 rs.u((uint32_t)(a.d - 1 - i)), WL, a.etab, dmu);
         if (o.z == kAmbZ) return kAmbiguous;
         zi = (double)o.z;
-        if (WL) lw += o.log_norm;
+        if (WL) {
+            lw += o.log_norm;
+            tb += fabs(o.log_norm);
+            const double rf = s < 0.1 ? (double)(a.precision > 3 ? a.precision : 3) : (double)a.precision;
+            if (dmu >= 0.0) eb += wl_bound_generic(o.log_norm, 1.0 / s, wl_window_hw(rf * s), dmu);
+        }
     }
     if (!WL) lw += ref_weight(zi, mu, cst(a.ros)[i], cst(a.isr)[i], cst(a.lterm)[i]);
     return zi;
@@ -157,7 +199,8 @@ struct RecView {  // q[k] of the SampleZ functions, served from the registers
 template <bool WL, bool CERT, bool LIBM, typename TP>
 __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, double mu,
                                                    lds_cdptr rec, const RecRegs& rr, CoordStream& rs, double& lw,
-                                                   unsigned int& flags, TP etab, double dmu, bool& amb) {
+                                                   unsigned int& flags, TP etab, double dmu, bool& amb,
+                                                   double& eb, double& tb) {
     double zi = 0.0;
     amb = false;
     if (!isfinite(mu)) {
@@ -190,7 +233,12 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
                                 rs.u((uint32_t)(a.d - 1 - i)), WL, a.etab, CERT ? dmu : -1.0);
         amb = CERT && o.z == kAmbZ;
         zi = amb ? rint(mu) : (double)o.z;
-        if (WL) lw += amb ? 0.0 : o.log_norm;
+        if (WL) {
+            const double ln = amb ? 0.0 : o.log_norm;
+            lw += ln;
+            tb += fabs(ln);
+            eb += amb ? 0.0 : wl_bound_generic(ln, qh.v[1], wl_window_hw(qh.v[6]), dmu);
+        }
     } else {
         // Inline one-dominant-point decision of the small kind (NTRU's sigma_i ~ 1e-3
         // coordinates), certified as in sample_z_coord_body: no call and no Philox
@@ -199,6 +247,7 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         // ends could add, has probability exactly 0 -- rec[7] == 0)
         bool fast = false;
         double ln = 0.0;
+        double ebf = 0.0;  // (WL) the fast decision's weight bound
         // the kind and its flag are the same in every lane: scalar branches
         const int kind = __builtin_amdgcn_readfirstlane((int)qh.v[2]);
         const int q7 = __builtin_amdgcn_readfirstlane(qh.v[7] == 0.0 ? 0 : (qh.v[7] == 1.0 ? 1 : 2));
@@ -216,6 +265,7 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
                    gap - 745.2 > 1.01 * dmu * hl * is2 + 1e-12 * gap;
             zi = c;
             ln = emax;
+            if (WL) ebf = wl_bound_dominant(emax, is2, d1, dmu);
         }
         if (!fast) {
             const double u = rs.u((uint32_t)(a.d - 1 - i));
@@ -245,8 +295,13 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
                 r = sample_z_coord_leaf<CERT>(mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, dmu);
             zi = sz_finish<CERT>(r, mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, ln, dmu, amb);
             }
+            if (WL) ebf = amb ? 0.0 : wl_bound_generic(ln, qh.v[1], wl_window_hw(qh.v[6]), dmu);
         }
-        if (WL) lw += ln;
+        if (WL) {
+            lw += ln;
+            tb += fabs(ln);
+            eb += ebf;
+        }
     }
     if (!WL) {
         const double t = ref_weight(zi, mu, rr[kRecRos], rr[kRecIsr], rr[kRecLterm]);
@@ -309,7 +364,7 @@ __device__ __noinline__ Resolved resolve_decision(const double* __restrict__ R, 
 
 template <bool WL, typename ZT>
 __device__ __forceinline__ double resolve_coord(const KleinArgs& a, int i, const ZT* Zp, size_t ldz,
-                                                CoordStream& rs, double& lw, unsigned int& flags) {
+                                                CoordStream& rs, double& lw, unsigned int& flags, double& tb) {
     const size_t iq = (size_t)i * kSzcStride;
     const Resolved r = resolve_decision(a.R, Zp, ldz, i, a.d, cst(a.cp)[i], cst(a.rii)[i],
                                         a.szc ? a.szc + iq : nullptr,
@@ -321,6 +376,7 @@ __device__ __forceinline__ double resolve_coord(const KleinArgs& a, int i, const
         return 0.0;
     }
     lw += WL ? r.ln : ref_weight(r.z, r.mu, cst(a.ros)[i], cst(a.isr)[i], cst(a.lterm)[i]);
+    if (WL) tb += fabs(r.ln);  // (a term at the reference-order mean: no bound)
     return r.z;
 }
 
@@ -394,6 +450,8 @@ struct VerifyOut {
     double lw;
     unsigned int flags;
     int nz;
+    double tabs;  // (WL) sum |term| of the terms it added (reference-order means: no bound)
+    double z2;    // sum z^2 of the calling lane's sub-panel after a replay of it, else -1
 };
 template <bool WL, bool OZ, typename ZT>
 __device__ __noinline__ VerifyOut verify_subpanel(KArgsPtr A, ZT* __restrict__ Z, size_t ldz,
@@ -401,6 +459,7 @@ __device__ __noinline__ VerifyOut verify_subpanel(KArgsPtr A, ZT* __restrict__ Z
                                                   uint32_t step, uint32_t chain, double* z1l,
                                                   const double* z1s, const double* lws, unsigned int flags) {
     int nz = 0;
+    double tabs = 0.0, z2 = -1.0;
     const int lane = threadIdx.x & 63;
     const int d = A->d;
     // the sub-panel's coefficients / history were just stored by their own lanes and
@@ -449,7 +508,7 @@ __device__ __noinline__ VerifyOut verify_subpanel(KArgsPtr A, ZT* __restrict__ Z
             }
         };
         bool full = (flL >> 16) & 1;
-        double dlw = 0.0;
+        double dlw = 0.0, dtb = 0.0;
         unsigned int fb = 0;
         for (int s = 0; s < rows && !full; ++s) {
             if (!((flL >> s) & 1)) continue;
@@ -459,8 +518,9 @@ __device__ __noinline__ VerifyOut verify_subpanel(KArgsPtr A, ZT* __restrict__ Z
             const double zi = decide(i, mu, term, fb);
             if (zi != guess(i)) full = true;
             else dlw += term;
+            dtb += fabs(term);
         }
-        double z1n = 0.0;
+        double z1n = 0.0, z2n = 0.0;
         int nzL = 0;
         if (full) {  // replay the sub-panel from its start
             dlw = 0.0;
@@ -471,7 +531,9 @@ __device__ __noinline__ VerifyOut verify_subpanel(KArgsPtr A, ZT* __restrict__ Z
                 double term;
                 const double zi = decide(i, mu, term, fb);
                 dlw += term;
+                dtb += fabs(term);
                 z1n += fabs(zi);
+                z2n = fma(zi, zi, z2n);
                 nzL |= zi != 0.0;
                 if (lane == L) {
                     store_z(Z, (size_t)i * ldz + pL, zi, fb);
@@ -488,9 +550,11 @@ __device__ __noinline__ VerifyOut verify_subpanel(KArgsPtr A, ZT* __restrict__ Z
         }
         if (lane == L) {
             flags |= fb;
+            tabs += dtb;
             if (full) {
                 lw = lws[L] + dlw;
                 z1l[L] = z1n;
+                z2 = z2n;
                 nz |= nzL;
             } else {
                 lw += dlw;
@@ -498,7 +562,7 @@ __device__ __noinline__ VerifyOut verify_subpanel(KArgsPtr A, ZT* __restrict__ Z
         }
         if (lane == 0) atomicAdd(A->flags + kFlagWordResolved, 1u);
     }
-    return VerifyOut{lw, flags, nz};
+    return VerifyOut{lw, flags, nz, tabs, z2};
 }
 
 // ------------------------------------------------------------ exact order
@@ -519,15 +583,17 @@ __global__ __launch_bounds__(256) void klein_exact_kernel(const KleinArgs a,
     const size_t ldz = (size_t)a.ldz;
     double lw = 0.0;
     unsigned int flags = 0;
+    double eb = 0.0, tb = 0.0;
     for (int i = d - 1; i >= 0; --i) {
         const double* __restrict__ Ri = R + (size_t)i * d;
         double cs = 0.0;
         for (int j = i + 1; j < d; ++j) cs = cs + Ri[j] * (double)Z[(size_t)j * ldz + p];
         const double mu = (a.cp[i] - cs) / a.rii[i];
-        const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s, -1.0);
+        const double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s, -1.0, eb, tb);
         store_z(Z, (size_t)i * ldz + p, zi, flags);
     }
     if (a.LW) a.LW[p] = lw;
+    if (a.LWE) a.LWE[p] = 0.0;  // the reference's order: exact
     if (flags) atomicOr(a.flags, flags);
 }
 
@@ -558,6 +624,7 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
     const int npan = (d + PB - 1) / PB;
     double acc[PB];
     double z1 = 0.0;  // sum of |z_j| decided so far (certificate)
+    double eb = 0.0, tb = 0.0;  // (WL) weight bound and sum |terms|
     for (int pk = 0; pk < npan; ++pk) {
         const int p_hi = d - pk * PB;
         const int rows = p_hi < PB ? p_hi : PB;
@@ -584,8 +651,8 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
             const int i = p_hi - 1 - s;
             const double mu = (cst(a.cp)[i] - acc[PB - 1]) * cst(a.irii)[i];
             double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s,
-                                         cert_dmu(cst(a.cert)[2 * i], cst(a.cert)[2 * i + 1], z1, mu));
-            if (zi == kAmbiguous) zi = resolve_coord<WL>(a, i, Z + p, ldz, rs, lw, flags);
+                                         cert_dmu(cst(a.cert)[2 * i], cst(a.cert)[2 * i + 1], z1, mu), eb, tb);
+            if (zi == kAmbiguous) zi = resolve_coord<WL>(a, i, Z + p, ldz, rs, lw, flags, tb);
             z1 += fabs(zi);
             store_z(Z, (size_t)i * ldz + p, zi, flags);
             const double x = zi;
@@ -598,6 +665,7 @@ __global__ __launch_bounds__(256) void klein_panel_kernel(const KleinArgs a,
         }
     }
     if (a.LW) a.LW[p] = lw;
+    if (WL) wl_bound_store(a, p, wl_bound_sum(eb, tb, d));
     if (flags) atomicOr(a.flags, flags);
 }
 
@@ -992,6 +1060,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
     constexpr int NACC = PB == 32 ? 16 : PB;  // running sums live across SampleZ calls
     double acc[NACC];
     double z1 = 0.0;  // sum of |z_j| decided so far (certificate; 16-row panels)
+    double eb = 0.0, tb = 0.0;  // (WL) weight bound and sum |terms| (wl_bound_*)
     // 32-row panels, per lane in LDS (a live register pair across the near field
     // measured 0.7 ms slower per 2^20 samples): [0] the running sum of |z_j|, [1] it
     // and [2] the weight at the start of the current sub-panel (for a replay)
@@ -999,18 +1068,50 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
     // bit s: decision s of the current sub-panel not covered by the certificate (in
     // LDS, written only when set: a live mask register costs ~13 scratch ops per
     // coordinate at this kernel's register pressure)
+#ifdef LGS_NEAR_UNROLLED
     __shared__ int cert_fl[PB == 32 ? 256 : 1];
+#else
+    __shared__ int cert_fl[1];
+#endif
+    // q-panel skip (reference mode, a.qz2): per lane sum z_j^2 over the coordinates
+    // outside speculative sub-panels (+inf once a speculative coordinate is nonzero),
+    // and the block's vote for skipping the current panel
+    __shared__ double qzs[PB == 32 ? 256 : 1];
+    __shared__ int qskip_blk;
     if constexpr (PB == 32) {
         cert_lds[0][threadIdx.x] = 0.0;
+#ifdef LGS_NEAR_UNROLLED
         cert_fl[threadIdx.x] = 0;
+#endif
+        qzs[threadIdx.x] = 0.0;
     }
     for (int pk = 0; pk < npan; ++pk) {
         const int p_hi = d - pk * PB;
         const int rows = p_hi < PB ? p_hi : PB;
         LGS_DC_T(t_panel0);
         if constexpr (PB == 32) {
+            // q-panel skip (reference mode): a panel of 32 small-kind rows whose means the
+            // host bounds by Cauchy-Schwarz, |mu_i| <= (|c'_i| + (1 + g) G_i ||z_W||) / R_ii
+            // (G_i = ||R[i, W]||, W = the coordinates outside speculative sub-panels, valid
+            // while every speculative z so far is 0), is decided z = 0 in every row with
+            // certainty when ||z_W||^2 <= qz2[pk] (the one-dominant-point test passes for
+            // every |mu| below the bound, lgs_set_basis): no far field, no means.  The
+            // weight term of such a row is taken at mu = 0: ref_weight(0, 0) = lterm
+            // exactly, against lterm + 0.5 mu^2 (isr^2 - ros^2) ~ lterm + 1e-15 at the
+            // blocked mean (isr and ros are R_ii / sigma in two roundings).  Block-wide
+            // (the far field stages the R-digit slab with block barriers).
+            bool qtry = false;
+#ifndef LGS_NEAR_UNROLLED  // (that variant does not track ||z_W||)
+            if constexpr (OZ && !WL)
+                qtry = a.qz2 != nullptr && p_hi >= 32 && ((const __attribute__((address_space(4))) double*)a.qz2)[pk] >= 0.0;
+#endif
             // records of coordinates r0 .. r0+31 (r0 = p_hi - 32; negative ones skipped)
+            if (qtry && threadIdx.x == 0) qskip_blk = 1;  // (every wave read the last panel's vote)
             __syncthreads();
+            if (qtry) {
+                const double q2 = ((const __attribute__((address_space(4))) double*)a.qz2)[pk];
+                if (__builtin_amdgcn_ballot_w64(active && !(qzs[threadIdx.x] <= q2)) != 0 && lane == 0) qskip_blk = 0;
+            }
             const int r0 = p_hi - 32;
             const double2* __restrict__ src = (const double2*)a.crec;
             double2* dst = (double2*)rec_lds;
@@ -1018,6 +1119,24 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                 if (r0 * (kRecStride / 2) + e >= 0) dst[e] = src[(int64_t)r0 * (kRecStride / 2) + e];
             __syncthreads();
             if (!active) continue;
+            if (qtry && __builtin_amdgcn_readfirstlane(qskip_blk) != 0) {
+#pragma unroll
+                for (int s = 0; s < 32; ++s) {
+                    Z[(size_t)(p_hi - 1 - s) * ldz + p] = (ZT)0;
+                    lw += ((lds_cdptr)rec_lds)[(31 - s) * kRecStride + kRecLterm];  // the sequential order
+                }
+                v4u_t* hp4 = (v4u_t*)(a.h16 + ((size_t)((p_hi - 32 + a.h16_shift) >> 4) * a.h16_lanes + p) * 16);
+                const v4u_t h128 = (v4u_t){0x00800080u, 0x00800080u, 0x00800080u, 0x00800080u};
+                hp4[0] = h128;
+                hp4[1] = h128;
+                hp4[(size_t)a.h16_lanes * 2] = h128;
+                hp4[(size_t)a.h16_lanes * 2 + 1] = h128;
+                if (a.znz) {
+                    a.znz[(size_t)((p_hi - 32 + a.h16_shift) >> 4) * a.h16_lanes + p] = 0;
+                    a.znz[(size_t)((p_hi - 16 + a.h16_shift) >> 4) * a.h16_lanes + p] = 0;
+                }
+                continue;
+            }
         }
         // Coarse panel (reference mode, both sub-panels speculative): the far field with
         // the kOzCoarse most significant R digits, certified with the matching bound
@@ -1174,7 +1293,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         bool un;
                         const double zi = decide_coord_rec<WL, true, LIBM>(a, i, mu, rec, rr, rs, lw, flags, etab_s,
                                                                      cert_dmu(rr[kSzCa], rr[kSzCb], a.z1cap, mu),
-                                                                     un);
+                                                                     un, eb, tb);
                         if (un) cert_fl[threadIdx.x] |= 1 << s;
 #ifdef LGS_DIAG_CYCLES
                         {
@@ -1256,6 +1375,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                                                                  &cert_lds[1][w64], &cert_lds[2][w64], flags);
                     lw = vo.lw;
                     flags = vo.flags;
+                    if (WL) tb += vo.tabs;
                     if constexpr (OZ) pnz |= vo.nz != 0;
                 }
                 if constexpr (OZ)  // (this variant keeps no per-sub-panel flag: the block counts as nonzero)
@@ -1281,6 +1401,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                 for (int j = 0; j < 8; ++j) hp[j] = 0u;
                 int flm = 0;
                 bool snz = false;  // (OZ) a nonzero z in this sub-panel, this lane
+                double zsq = 0.0;  // (q-panel skip) sum z^2 of this sub-panel, this lane
                 typedef double d2v __attribute__((ext_vector_type(2)));
 #ifndef LGS_NEAR_UNROLL  // coordinates per loop iteration (the running sums shift by one per step)
 #define LGS_NEAR_UNROLL 1
@@ -1296,7 +1417,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     bool un;
                     const double zi = decide_coord_rec<WL, true, LIBM>(
                         a, i, mu, rec, rr, rs, lw, flags, etab_s,
-                        cert_dmu(rr[kSzCa], coarse ? rec[kRecCbC] : rr[kSzCb], a.z1cap, mu), un);
+                        cert_dmu(rr[kSzCa], coarse ? rec[kRecCbC] : rr[kSzCb], a.z1cap, mu), un, eb, tb);
                     flm |= un ? (1 << s) : 0;
 #ifdef LGS_DIAG_CYCLES
                     {
@@ -1327,6 +1448,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         } else {
                             const int ih = i + a.h16_shift;
                             a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] = (int16_t)hv;
+                            if constexpr (!WL) zsq = fma(zi, zi, zsq);  // (whole sub-panels: from hp below)
                         }
                         snz |= zi != 0.0;
                     }
@@ -1340,6 +1462,15 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         v4u_t* hp4 = (v4u_t*)(a.h16 + ((size_t)((top - 16 + a.h16_shift) >> 4) * a.h16_lanes + p) * 16);
                         hp4[0] = (v4u_t){hp[0], hp[1], hp[2], hp[3]};
                         hp4[1] = (v4u_t){hp[4], hp[5], hp[6], hp[7]};
+                        if constexpr (!WL) {  // sum z^2 of the sub-panel from its packed history (z + 128)
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) {
+                                const double zl = (double)((int)(hp[j] & 0xffffu) - 128);
+                                const double zh = (double)((int)(hp[j] >> 16) - 128);
+                                zsq = fma(zl, zl, zsq);
+                                zsq = fma(zh, zh, zsq);
+                            }
+                        }
                     }
                 }
                 // the certificate used sum_{j>i} |z_j| <= z1cap: verify it (the sum at the
@@ -1353,11 +1484,23 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                                                                  &cert_lds[1][w64], &cert_lds[2][w64], flags);
                     lw = vo.lw;
                     flags = vo.flags;
+                    if (WL) tb += vo.tabs;
                     if constexpr (OZ) snz |= vo.nz != 0;
+                    if (vo.z2 >= 0.0) zsq = vo.z2;
+                }
+                if constexpr (OZ && !WL) {  // the q-panel skip's ||z_W||^2 (+inf: a speculative z != 0)
+                    const bool spec_sp = rows16 == 16 &&
+                                         __builtin_amdgcn_readfirstlane((int)((lds_cdptr)rec_lds)[(top - 1 - (p_hi - 32)) * kRecStride + kRecSpec]) == 1;
+                    qzs[threadIdx.x] = spec_sp ? (zsq != 0.0 ? __builtin_inf() : qzs[threadIdx.x]) : qzs[threadIdx.x] + zsq;
                 }
                 if constexpr (OZ) {
                     pnz |= snz;
                     if (a.znz) a.znz[(size_t)((top - 1 + a.h16_shift) >> 4) * a.h16_lanes + p] = snz ? 1 : 0;
+                    // the wave's 64-coordinate chunk of these rows holds a nonzero (B z skips
+                    // the others with one word per 32 chunks, not one flag load per chunk)
+                    if (a.clive && top >= 16 && __builtin_amdgcn_ballot_w64(snz) != 0 && lane == 0)
+                        atomicOr(a.clive + (size_t)((top - 16) >> 11) * a.clive_ld + (p0 >> 6),
+                                 1u << (((top - 16) >> 6) & 31));
                 }
             };
             // one copy of the 16-step near field for both sub-panels (a second inlined
@@ -1423,6 +1566,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     // sub-panel 0 that sum is the one at its start (else: the sequential
                     // path, whose end-of-sub-panel check verifies)
                     bool ok = cert_lds[0][threadIdx.x] <= a.z1cap;
+                    double ebs = 0.0;  // (WL) the sub-panel's weight bound
 #pragma unroll
                     for (int s = 0; s < 16; ++s) {
                         const lds_cdptr rec = (lds_cdptr)rec_lds + (top - 1 - s - (p_hi - 32)) * kRecStride;
@@ -1437,10 +1581,16 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                                           gap - 745.2 > 1.01 * dmu * hl * is2 + 1e-12 * gap;
                         ok = ok && isfinite(mu) && fast && c == 0.0;
                         term[s] = WL ? emax : ref_weight(c, mu, rec[kRecRos], rec[kRecIsr], rec[kRecLterm]);
+                        if (WL) ebs += wl_bound_dominant(emax, is2, d1, dmu);
                     }
                     if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
 #pragma unroll
                         for (int s = 0; s < 16; ++s) lw += term[s];  // the sequential order
+                        if (WL) {
+#pragma unroll
+                            for (int s = 0; s < 16; ++s) tb += fabs(term[s]);
+                            eb += ebs;
+                        }
 #pragma unroll
                         for (int s = 0; s < 16; ++s) Z[(size_t)(top - 1 - s) * ldz + p] = (ZT)0;
                         if constexpr (OZ) {  // int16 history: z + 128 in all 16 positions
@@ -1470,8 +1620,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                 const int i = p_hi - 1 - s;
                 const double mu = (cst(a.cp)[i] - acc[PB - 1]) * cst(a.irii)[i];
                 double zi = decide_coord<WL>(a, i, mu, rs, lw, flags, etab_s,
-                                             cert_dmu(cst(a.cert)[2 * i], cst(a.cert)[2 * i + 1], z1, mu));
-                if (zi == kAmbiguous) zi = resolve_coord<WL>(a, i, Z + p, ldz, rs, lw, flags);
+                                             cert_dmu(cst(a.cert)[2 * i], cst(a.cert)[2 * i + 1], z1, mu), eb, tb);
+                if (zi == kAmbiguous) zi = resolve_coord<WL>(a, i, Z + p, ldz, rs, lw, flags, tb);
                 z1 += fabs(zi);
                 store_z(Z, (size_t)i * ldz + p, zi, flags);
                 const double x = zi;
@@ -1490,8 +1640,17 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
         for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o));
         if (lane == 0 && a.z1max) atomicMax(a.z1max, (unsigned long long)__double_as_longlong(m));
     }
+    const double ewl = WL ? wl_bound_sum(eb, tb, d) : 0.0;
+    if (WL && PB == 32 && a.emax) {  // the wave's largest weight bound -> the context's running maximum
+        double m = active ? ewl : 0.0;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+        if (lane == 0) atomicMax(a.emax, (unsigned long long)__double_as_longlong(m));
+    }
     if (!active) return;
     if (a.LW) a.LW[p] = lw;
+    if (WL && PB == 32 && a.LWE) a.LWE[p] = ewl;
+    if (WL && PB != 32) wl_bound_store(a, p, ewl);
     if (flags) atomicOr(a.flags, flags);
 #ifdef LGS_DIAG_CYCLES
     LGS_DC_T(t_kernel1);
@@ -1597,6 +1756,215 @@ __global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
             ++keep;
         }
     }
+    a.lw_state[c] = lw_x;
+    a.accepts[c] += acc;
+    a.final_sel[c] = cur;
+    if (a.cnt_carry) a.cnt_carry[c] = carry;
+}
+
+// ------------------------------------------------- certified Wang-Ling decisions
+// The blocked kernels' Wang-Ling weights are within LWE of the reference-order
+// values (wl_bound_*).  A decision u < min(1, exp(lw_y - lw_x)) (imhk.py:158-167) is
+// taken at those weights only when it is the same for every pair within the
+// bounds; otherwise the wave recomputes both weights in the reference's order
+// (wl_exact_wave) and decides at them -- the decision klein_exact_kernel's weights
+// give.  Chain states carried into a block have the bound *emax (the context's
+// running maximum over its Wang-Ling draws).
+
+__device__ __forceinline__ double readlane_f64(double v, int k) {
+    const long long b = __double_as_longlong(v);
+    return __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(b >> 32), k) << 32) |
+                                (unsigned int)__builtin_amdgcn_readlane((int)b, k));
+}
+__device__ __forceinline__ double zload(const void* base, int zb, int64_t off) {
+    if (zb == 2) return (double)((const int16_t*)base)[off];
+    if (zb == 4) return (double)((const int32_t*)base)[off];
+    return (double)((const int64_t*)base)[off];
+}
+
+// decide_coord's draw and Wang-Ling term at mean mu, for a coordinate i that may
+// differ between lanes (global-pointer SampleZ constants: no uniformisation)
+__device__ __forceinline__ double wl_decide_lane(const KleinArgs& a, int i, double mu, double u, double& ln) {
+    ln = 0.0;
+    if (!isfinite(mu)) return 0.0;
+    const double s = a.szc ? a.szc[(size_t)i * kSzcStride] : a.sig[i];
+    if (s == 0.0) return rint(mu);
+    if (a.szc)
+        return sample_z_coord(mu, u, (gdptr)(a.szc + (size_t)i * kSzcStride), a.precision, a.linear_probs != 0,
+                              true, (gdptr)a.etab, ln, -1.0);
+    const SampleZOut o = sample_z(mu, s, a.precision, a.linear_probs != 0, u, true, a.etab);
+    ln = o.log_norm;
+    return (double)o.z;
+}
+
+// Wang-Ling log weight of ONE sample in the reference's arithmetic order -- what
+// klein_exact_kernel returns for it: the means (c'_i - sum_{j>i} R_ij z_j) / R_ii
+// with the j-ascending unfused sum of klein.py:191-195, each coordinate's window
+// normaliser at its mean (decide_coord's SampleZ call, same uniform), added for
+// i = d-1 .. 0.  Whole wave, uniform arguments.  Lane k owns coordinates k + 64 m
+// (16 per pass, so d > 1024 takes several passes, top rows first); z_j is broadcast
+// (zero terms skipped: cs + R * (+-0) = cs, cs is never -0), R is read through its
+// transpose (one coalesced row segment per m).  z_j at zsrc[j * zst], width zb.
+// check: the draws at those means must reproduce z (the sample's own counters).
+__device__ double wl_exact_wave(const KleinArgs& a, const double* __restrict__ RT, const void* zsrc, int zb,
+                                int64_t zst, uint32_t step, uint32_t chain, bool check, int& bad) {
+    const int lane = threadIdx.x & 63;
+    const int d = a.d;
+    constexpr int MB = 16;
+    const int M = (d + 63) / 64;
+    CoordStreamT<false> rs;
+    rs.init(a.seed, step, chain);
+    double lw = 0.0;
+    for (int mb = (M - 1) / MB * MB; mb >= 0; mb -= MB) {
+        const int ilo = 64 * mb;
+        double cs[MB];
+#pragma unroll
+        for (int m = 0; m < MB; ++m) cs[m] = 0.0;
+        for (int j0 = ilo; j0 < d; j0 += 64) {
+            const double zv = j0 + lane < d ? zload(zsrc, zb, (int64_t)(j0 + lane) * zst) : 0.0;
+            const int jn = min(64, d - j0);
+            for (int k = 0; k < jn; ++k) {
+                const double zj = readlane_f64(zv, k);
+                if (zj == 0.0) continue;
+                const int j = j0 + k;
+                const double* __restrict__ rt = RT + (size_t)j * d + ilo + lane;
+#pragma unroll
+                for (int m = 0; m < MB; ++m)
+                    if (ilo + 64 * m + lane < j) cs[m] = cs[m] + rt[64 * m] * zj;
+            }
+        }
+        double lnv[MB];
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+            const int i = ilo + 64 * m + lane;
+            lnv[m] = 0.0;
+            if (i < d) {
+                const double mu = (a.cp[i] - cs[m]) / a.rii[i];
+                const double zi = wl_decide_lane(a, i, mu, rs.u((uint32_t)(d - 1 - i)), lnv[m]);
+                if (check && zi != zload(zsrc, zb, (int64_t)i * zst)) bad = 1;
+            }
+        }
+#pragma unroll
+        for (int m = MB - 1; m >= 0; --m) {
+            if (ilo + 64 * m >= d) continue;
+            for (int k = 63; k >= 0; --k)
+                if (ilo + 64 * m + k < d) lw = lw + readlane_f64(lnv[m], k);
+        }
+    }
+    return lw;
+}
+
+__device__ __forceinline__ double accept_ratio(double lw_y, double lw_x) {
+    if (lw_x == -INFINITY) return 1.0;
+    const double r = exp(lw_y - lw_x);
+    return r < 1.0 ? r : 1.0;  // min(1.0, r); NaN -> 1.0 like Python's min
+}
+// true when u < min(1, exp(lw_y' - lw_x')) is the same for every |lw_x' - lw_x| <= e_x,
+// |lw_y' - lw_y| <= e_y (take: the decision).  The difference of the two computed
+// differences is <= e_x + e_y + 2u(|lw_x| + |lw_y|); exp is monotone to within its
+// ~1 ulp error (the 1e-15 factors).
+__device__ __forceinline__ bool accept_certain(double lw_x, double e_x, double lw_y, double e_y, double u,
+                                               bool& take) {
+    take = u < accept_ratio(lw_y, lw_x);
+    if (e_x == 0.0 && e_y == 0.0) return true;
+    if (!isfinite(lw_x) || !isfinite(lw_y)) return false;
+    const double D = lw_y - lw_x;
+    const double eps = e_x + e_y + 2.3e-16 * (fabs(lw_x) + fabs(lw_y));
+    const double rlo = fmin(1.0, exp(D - eps) * (1.0 - 1e-15));
+    const double rhi = fmin(1.0, exp(D + eps) * (1.0 + 1e-15));
+    return u < rlo || u >= rhi;
+}
+
+// imhk_accept_kernel with certified decisions (AcceptArgs.LWE non-null): one wave
+// per block, every lane stays to the end (the rare recomputation needs the whole
+// wave); lanes beyond nc write nothing.
+__global__ __launch_bounds__(64) void imhk_accept_cert_kernel(const AcceptArgs a, const KleinArgs ka) {
+    if (aborted(a.abort)) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t c0 = (int64_t)blockIdx.x * 64;
+    const int64_t c = c0 + lane;
+    const bool live = c < a.nc;
+    double lw_x = live ? a.lw_state[c] : 0.0;
+    double e_x = a.bscale * __longlong_as_double((long long)*(const volatile unsigned long long*)a.emax);
+    int64_t cur = -1;
+    int64_t acc = 0;
+    int64_t keep = 0;
+    int32_t carry = 0;
+    unsigned int nres = 0;
+    int bad = 0;
+    const uint32_t chain = a.chain0 + (uint32_t)c;
+    for (int64_t t = 0; t < a.T; ++t) {
+        const int64_t p = c * a.T + t;
+        double lw_y = live ? a.LWx[p] : 0.0;
+        double e_y = live ? a.bscale * a.LWE[p] : 0.0;
+        const double u = accept_uniform(a.seed, a.step0 + (uint32_t)t, chain);
+        bool take = false;
+        const bool sure = !live || accept_certain(lw_x, e_x, lw_y, e_y, u, take);
+        uint64_t todo = __builtin_amdgcn_ballot_w64(!sure);
+        while (todo) {  // rare: reference-order weights of lane L's proposal and state
+            const int L = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const int64_t cL = c0 + L;
+            const uint32_t chL = a.chain0 + (uint32_t)cL;
+            const double eyL = readlane_f64(e_y, L), exL = readlane_f64(e_x, L);
+            const int64_t curL = ((int64_t)__builtin_amdgcn_readlane((int)(cur >> 32), L) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)cur, L);
+            double ly = 0.0, lx = 0.0;
+            if (eyL != 0.0)
+                ly = wl_exact_wave(ka, a.RT, (const char*)a.Zst + (cL * a.T + t) * a.zb, a.zb, a.ldz,
+                                   a.step0 + (uint32_t)t, chL, true, bad);
+            if (exL != 0.0) {
+                if (curL >= 0)  // an earlier proposal of this block
+                    lx = wl_exact_wave(ka, a.RT, (const char*)a.Zst + curL * a.zb, a.zb, a.ldz,
+                                       a.step0 + (uint32_t)(curL % a.T), chL, true, bad);
+                else  // the state carried in (its counters are not known: the uniforms only
+                      // select the rare table-walk path, whose normaliser agrees to ~1e-13)
+                    lx = wl_exact_wave(ka, a.RT,
+                                       (const char*)a.zs + (a.zs_cm ? cL : cL * ka.d) * a.ob, a.ob,
+                                       a.zs_cm ? a.nc : 1, 0u, chL, false, bad);
+            }
+            if (lane == L) {
+                if (eyL != 0.0) {
+                    lw_y = ly;
+                    e_y = 0.0;
+                    a.LWx[p] = ly;
+                    a.LWE[p] = 0.0;
+                }
+                if (exL != 0.0) {
+                    lw_x = lx;
+                    e_x = 0.0;
+                    if (cur >= 0) {
+                        a.LWx[cur] = lx;
+                        a.LWE[cur] = 0.0;
+                    }
+                }
+                take = u < accept_ratio(lw_y, lw_x);
+                ++nres;
+            }
+        }
+        if (!live) continue;
+        if (take) {
+            cur = p;
+            lw_x = lw_y;
+            e_x = e_y;
+            ++acc;
+        }
+        if (a.acc_step) a.acc_step[c * a.acc_ld + t] = take ? 1 : 0;
+        if ((t + 1) % a.thin == 0) {
+            if (a.lw_keep) a.lw_keep[c * a.lw_ld + keep] = lw_x;
+            if (a.sel) a.sel[c * a.n_keep + keep] = cur >= 0 ? cur : (a.carry_col >= 0 ? a.carry_col + c : -1);
+            if (a.cnt) {
+                if (cur < 0)
+                    ++carry;
+                else
+                    a.cnt[cur] += 1;
+            }
+            ++keep;
+        }
+    }
+    if (nres) atomicAdd(a.flagw + kFlagWordAcceptResolved, nres);
+    if (__builtin_amdgcn_ballot_w64(bad != 0) != 0 && lane == 0) atomicAdd(a.flagw + kFlagWordWLMismatch, 1u);
+    if (!live) return;
     a.lw_state[c] = lw_x;
     a.accepts[c] += acc;
     a.final_sel[c] = cur;
@@ -2004,7 +2372,8 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
                                                     unsigned int* flags, int tx_count, int64_t ty_count,
                                                     const int16_t* __restrict__ h16, int64_t h16_lanes,
                                                     int64_t hcols, const unsigned int* abort,
-                                                    const uint8_t* __restrict__ znz) {
+                                                    const uint8_t* __restrict__ znz,
+                                                    const unsigned int* __restrict__ clive, int64_t clive_ld) {
     if (aborted(abort)) return;  // (whole grid) the selections were not written
     constexpr int TA = LGS_BZ_TA;  // 32-sample MFMA tiles per wave
     constexpr int BM = 64 * TA, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
@@ -2053,8 +2422,25 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
     // block zq of each chunk for its sample, the tile ORs them in LDS.  Samples read
     // from the coefficient store (not that launch's) count as nonzero.  (NTRU / q-ary
     // bases: the q-coordinates' z are 0, which leaves ~1 of 6 chunks per tile.)
-    const bool use_znz = KPT == 16 && h16 != nullptr && znz != nullptr;
+    // (round 4) the Klein launch also leaves, per wave, one bit per 64-coordinate chunk
+    // (clive): the tile's live chunks are the OR of its samples' waves' words -- one
+    // load per 32 chunks and sample instead of one flag load and LDS atomic per chunk
+    const bool use_clive = KPT == 16 && h16 != nullptr && clive != nullptr;
+    const bool use_znz = !use_clive && KPT == 16 && h16 != nullptr && znz != nullptr;
     __shared__ unsigned int livew[kOzMaxD / 64 / 32];
+    if (use_clive) {
+        if (wave == 0) {  // threads tid < 64: zq = 0, one sample per lane
+            const int ng = (d + 2047) / 2048;
+            for (int g = 0; g < ng; ++g) {
+                unsigned int w = 0u;
+                if (zs_ < n) w = zcol < hcols ? clive[(size_t)g * clive_ld + (zcol >> 6)] : 0xffffffffu;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) w |= __shfl_xor(w, o);
+                if (lane == 0) livew[g] = w;
+            }
+        }
+        __syncthreads();
+    }
     if (use_znz) {
         const bool hp = zs_ < n && zcol < hcols;
         for (int w = tid; w < (ci1 - ci0 + 31) / 32; w += 256) livew[w] = 0u;
@@ -2067,8 +2453,10 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
         __syncthreads();
     }
     for (int ci = ci0; ci < ci1; ++ci) {
+        const int cix = kchunk[ci];
+        if (use_clive && !((livew[cix >> 5] >> (cix & 31)) & 1u)) continue;  // (uniform)
         if (use_znz && !((livew[(ci - ci0) >> 5] >> ((ci - ci0) & 31)) & 1u)) continue;  // (uniform)
-        const int c0 = kchunk[ci] * KC;
+        const int c0 = cix * KC;
         if (KPT == 16 && h16 != nullptr && zs_ < n && zcol < hcols) {
             // column written by the Klein launch whose int16 history (z + 128,
             // [coordinate / 16][lane][16]) holds this sample's 16 coefficients in 32
@@ -2297,9 +2685,12 @@ hipError_t samplez_probe(const double* mu, const double* sig, const double* u, i
     return hipGetLastError();
 }
 
-hipError_t accept(const AcceptArgs& a, hipStream_t st) {
+hipError_t accept(const AcceptArgs& a, const KleinArgs& ka, hipStream_t st) {
     if (a.nc <= 0) return hipSuccess;
-    hipLaunchKernelGGL(imhk_accept_kernel, dim3((unsigned)((a.nc + 255) / 256)), dim3(256), 0, st, a);
+    if (a.LWE)
+        hipLaunchKernelGGL(imhk_accept_cert_kernel, dim3((unsigned)((a.nc + 63) / 64)), dim3(64), 0, st, a, ka);
+    else
+        hipLaunchKernelGGL(imhk_accept_kernel, dim3((unsigned)((a.nc + 255) / 256)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
@@ -2433,17 +2824,22 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
-                 hipStream_t st, const unsigned int* abort, const uint8_t* znz) {
+                 hipStream_t st, const unsigned int* abort, const uint8_t* znz, const unsigned int* clive,
+                 int64_t clive_ld) {
     if (n <= 0) return hipSuccess;
     if (d % 16 != 0 || LGS_BZ_TA != 1 || d > kOzMaxD) h16 = nullptr;  // history blocks must align with the chunks
 #ifdef LGS_BZ_NO_ZNZ
     znz = nullptr;
 #endif
     if (h16 == nullptr) znz = nullptr;
+    if (h16 == nullptr) clive = nullptr;
+#ifdef LGS_BZ_NO_CLIVE
+    clive = nullptr;
+#endif
     const int tx = ((d + 127) / 128 + LGS_BZ_TXPER - 1) / LGS_BZ_TXPER;  // coordinate-tile groups
     const int64_t ty = (n + 64 * LGS_BZ_TA - 1) / (64 * LGS_BZ_TA);
     const dim3 grid((unsigned)(tx * ((ty + 7) / 8) * 8));  // whole rounds of 8 XCDs (extra tiles exit)
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort, znz));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort, znz, clive, clive_ld));
     return hipGetLastError();
 }
 

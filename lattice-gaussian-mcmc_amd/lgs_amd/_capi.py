@@ -31,6 +31,7 @@ LGS_COORD_MAJOR = 0x10
 LGS_SAMPLEZ_TABLE = 0x20
 LGS_SAMPLEZ_DECISION = 0x40
 LGS_SAMPLEZ_LIBM = 0x80
+LGS_LOGW_BOUND = 0x400
 
 LGS_X_I32 = 0x100
 LGS_X_I64 = 0x200
@@ -39,6 +40,8 @@ KERNEL_KLEIN, KERNEL_BZ, KERNEL_ACCEPT, KERNEL_MOMENTS = 0, 1, 2, 3
 KERNEL_GRAM, KERNEL_SERIES, KERNEL_KLEIN_INIT = 4, 5, 6
 LGS_COUNTER_RESOLVED = 0
 LGS_COUNTER_FALLBACK = 1
+LGS_COUNTER_ACCEPT_RESOLVED = 2
+LGS_COUNTER_WL_MISMATCH = 3
 
 # every symbol include/lgs.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_destroy", "lgs_set_stream",
@@ -404,6 +407,12 @@ class Context:
         """Klein launches redone with a wider store / the fp64 far field (LGS_COUNTER_FALLBACK)."""
         v = ctypes.c_uint64(0)
         _check(_lib.lgs_counter(self._h, LGS_COUNTER_FALLBACK, 1 if reset else 0, ctypes.byref(v)))
+        return v.value
+
+    def counter(self, which, reset=False):
+        """lgs_counter: one of the LGS_COUNTER_* event counts since creation / the last reset."""
+        v = ctypes.c_uint64(0)
+        _check(_lib.lgs_counter(self._h, int(which), 1 if reset else 0, ctypes.byref(v)))
         return v.value
 
     def device_info(self):

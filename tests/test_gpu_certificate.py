@@ -72,11 +72,13 @@ def test_speculative_small_kind_subpanels(capi, oracle, cfg, center_scale, wl):
     n = 1 << 14
     za = torch.empty((d, n), dtype=torch.int32, device="cuda")
     zb = torch.empty_like(za)
-    la = torch.empty(n, dtype=torch.float64, device="cuda")
-    lb = torch.empty_like(la)
-    f = capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR | (capi.LGS_WANG_LING if wl else 0)
-    ctx.klein(91, 0, n, za, None, la, f)
-    ctx.klein(91, 0, n, zb, None, lb, f | capi.LGS_EXACT_ORDER)
+    la2 = torch.empty(2 * n, dtype=torch.float64, device="cuda")  # weights, then their bounds
+    la, ea = la2[:n], la2[n:]
+    lb2 = torch.empty_like(la2)
+    lb, eb = lb2[:n], lb2[n:]
+    f = capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR | (capi.LGS_WANG_LING | capi.LGS_LOGW_BOUND if wl else 0)
+    ctx.klein(91, 0, n, za, None, la2 if wl else la, f)
+    ctx.klein(91, 0, n, zb, None, lb2 if wl else lb, f | capi.LGS_EXACT_ORDER)
     torch.cuda.synchronize()
     small = torch.as_tensor(np.flatnonzero(sigma / np.diag(R) < 4.0), device="cuda")  # the q-coordinates
     assert small.numel() >= d // 4
@@ -91,12 +93,17 @@ def test_speculative_small_kind_subpanels(capi, oracle, cfg, center_scale, wl):
     rel = float((dif / lb.abs().clamp_min(1.0)).max())
     print(f"  log weights: max difference {float(dif.max()):.2e}, relative {rel:.2e}")
     # Reference mode: the weight terms cancel to rounding.  Wang-Ling: the normaliser
-    # of a sigma_i ~ 1e-3 coordinate moves by |mu - rint(mu)| / sigma_i^2 ~ 1e4 per
-    # unit of mean, and the default kernels' means carry the far field's rounding of R
-    # to 48 bits of its row maximum (covered by the certificate for z, not for the
-    # weight): |dlw| <= 7e-6 at C3 (|lw| up to ~4e3, some samples near 0), DESIGN.md §7
+    # of a sigma_i ~ 1e-2 coordinate moves by |mu - rint(mu)| / sigma_i^2 per unit of
+    # mean, and the default kernels' means are within the certificate's dmu of the
+    # reference-order ones: every sample's weight must lie within the bound the kernel
+    # derives from those dmu (lgs_kernels.hip wl_bound_*, LGS_LOGW_BOUND); the
+    # reference-order kernel reports bound 0.  The accept decisions are certified
+    # against these bounds (test_gpu_wl_accept.py).
     if wl:
-        assert float(dif.max()) < 2e-5
+        assert float(eb.abs().max()) == 0.0
+        assert bool((dif <= ea).all()), float((dif - ea).max())
+        print(f"  bounds: median {float(ea.median()):.2e}, max {float(ea.max()):.2e}; "
+              f"max |dlw| / bound {float((dif / ea.clamp_min(1e-300)).max()):.3f}")
     else:
         assert rel < 1e-10
 
@@ -138,3 +145,38 @@ def test_low_z1_cap_forces_verification_not_speculation(capi, oracle, scale, mon
         assert redos >= n // 64  # every wave verified (cap below every sum)
     assert int((za != zb).any(dim=0).sum()) == 0
     assert float(((la - lb).abs() / lb.abs().clamp_min(1.0)).max()) < 1e-10
+
+
+@pytest.mark.parametrize("cfg,center_scale", [("C3_ntru512", 0.0), ("C3_ntru512", 3e4), ("C5_ntru2048", 0.0)])
+def test_q_panel_skip_equals_full_computation(capi, oracle, cfg, center_scale, monkeypatch):
+    """Reference mode skips a panel of speculative (tiny-sigma) rows when the host's
+    Cauchy-Schwarz bound on every row's mean, from ||z_W|| of the sample, certifies
+    z = 0 there (lgs_set_basis, klein_mfma_kernel).  z must equal the launch that
+    computes those panels (LGS_NO_QSKIP=1) and the reference-order kernel; the weights
+    differ by the rows' mean-dependent rounding only (the terms are lterm at mu = 0).
+    A center of scale ~q moves the means off 0: the bound fails and nothing is skipped."""
+    import torch
+    from lgs_amd.lattices import build_config
+    lat, sigma = build_config(cfg)
+    B = lat.basis
+    d = B.shape[0]
+    center = np.random.default_rng(5).uniform(-center_scale, center_scale, d) if center_scale else None
+    R, cp = oracle.qr_prepare(B, center)
+    n = 1 << 14 if d <= 1024 else 1 << 12
+    out = {}
+    for skip in ("0", "1"):
+        monkeypatch.setenv("LGS_NO_QSKIP", skip)
+        ctx = capi.Context(0)
+        ctx.set_basis(R, cp, B, sigma)
+        z = torch.empty((d, n), dtype=torch.int32, device="cuda")
+        lw = torch.empty(n, dtype=torch.float64, device="cuda")
+        ctx.timing_enable(True)
+        ctx.klein(17, 3 << 20, n, z, None, lw, capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR)
+        ms, _ = ctx.timing_get(capi.KERNEL_KLEIN)
+        out[skip] = (z, lw, ms)
+    ctx.klein(17, 3 << 20, n, out["1"][0], None, None, capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR | capi.LGS_EXACT_ORDER)
+    torch.cuda.synchronize()
+    print(f"{cfg} center {center_scale}: skip {out['0'][2]:.3f} ms, no skip {out['1'][2]:.3f} ms")
+    assert torch.equal(out["0"][0], out["1"][0])  # skipped panels: the same z as computed ones
+    rel = float(((out["0"][1] - out["1"][1]).abs() / out["1"][1].abs().clamp_min(1.0)).max())
+    assert rel < 1e-12, rel

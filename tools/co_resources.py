@@ -51,8 +51,9 @@ def kernels(lib):
 
 
 def waves_per_simd(r, block=256):
-    v = r.get("vgpr_count", 0) + r.get("agpr_count", 0)
-    # unified register file: 512 per lane per SIMD, allocation granule 8
+    # .vgpr_count is the unified total (arch VGPRs + AGPRs, gfx90a+): 512 per lane per
+    # SIMD, allocation granule 8
+    v = r.get("vgpr_count", 0)
     vg = 512 // max(8, -(-v // 8) * 8) if v else 8
     lds = r.get("group_segment_fixed_size", 0)
     wpb = max(1, -(-r.get("max_flat_workgroup_size", block) // 64))
