@@ -8,10 +8,14 @@ sigma = 165.7, IMHK with 2^14 chains per GPU.  One bench step = one
 Metropolis scan, exact integer moments, and the lattice points v = B z of every
 kept state (thin = 1), all resident in HBM; then the lag-L autocovariance sums
 of two scalar functionals of the kept states (a coefficient and ||v||^2, SURVEY
-§8e) are accumulated on the device.  The coefficient is z_{d-1}, the first one
-Klein decides (for the NTRU / q-ary bases z_0 is a q-coordinate with sigma_0 ~
-0.01, identically 0).  value = Klein proposals per second over all ranks
-(weak scaling: chains per GPU fixed).
+§8e) are accumulated on the device, both produced by the library itself
+(lgs_imhk_ex: ||v||^2 in the B z epilogue, the coefficient from the proposal
+store), and the exact sum z z^T of the chains' states after the step (lgs_gram;
+the job's empirical covariance, base.py:154-160, comes back from the same single
+all-reduce).  The coefficient is z_{d-1}, the first one Klein decides (for the
+NTRU / q-ary bases z_0 is a q-coordinate with sigma_0 ~ 0.01, identically 0).
+value = Klein proposals per second over all ranks (weak scaling: chains per GPU
+fixed).
 
 Multi-GPU: ``python bench.py --gpus N`` (no WORLD_SIZE in the environment)
 starts ``torch.distributed.run`` with N ranks as a child process and exits with

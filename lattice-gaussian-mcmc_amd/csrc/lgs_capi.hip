@@ -79,6 +79,7 @@ struct BzCall {  // an int8-digit B z launch, replayed in fp64 if a digit overfl
     double* V;
     int64_t rb, rstride, roff;
     const int64_t* sel;  // nullable: sample s reads column sel[s] of Z
+    double* VN;          // nullable: ||v||^2 of each row (same row index, ld 1)
 };
 
 }  // namespace
@@ -106,6 +107,7 @@ struct lgs_ctx {
     DevBuf QZ2;            // per 32-row panel: the q-panel skip's bound on ||z_W||^2 (klein_mfma_kernel)
     bool has_qz2 = false;
     uint64_t n_accept_resolved = 0, n_wl_mismatch = 0;
+    uint64_t n_qskip = 0;  // (wave, panel) pairs decided by the q-panel skip
     uint64_t n_fallback = 0;      // Klein launches redone with a wider store / fp64 far field
     // 32-row-panel kernels: the certificate's bound on sum_j |z_j| of a sample (an
     // estimate from the basis, then twice the largest sum seen; a sample exceeding it
@@ -117,6 +119,7 @@ struct lgs_ctx {
     DevBuf H16, F0;               // int8-digit far field scratch: coefficient history, tile-0 sums
     DevBuf ZNZ;                   // per history block and lane: any nonzero z (B z's chunk skipping)
     DevBuf CLIVE;                 // per wave and 64-coordinate chunk: any nonzero z (bits; B z)
+    DevBuf VNP;                   // B z's per-tile partial sums of ||v||^2 (lgs_imhk_ex vnorm2_samples)
     // the last Klein launch's history, valid for columns [0, cols) of the store Z it
     // wrote (B z reads its digits from there); reset by every Klein launch
     struct {
@@ -260,7 +263,7 @@ int finish(lgs_ctx* c, const unsigned int* fw_known = nullptr) {  // sync, fold 
         c->pool.push_back(t.b);
     }
     c->pending.clear();
-    unsigned int fw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned int fw[lgs::kFlagWords] = {};
     if (fw_known)
         memcpy(fw, fw_known, sizeof(fw));
     else
@@ -271,8 +274,12 @@ int finish(lgs_ctx* c, const unsigned int* fw_known = nullptr) {  // sync, fold 
         fold_counters(c, fw);
     c->n_accept_resolved += fw[lgs::kFlagWordAcceptResolved];
     c->n_wl_mismatch += fw[lgs::kFlagWordWLMismatch];
-    if (fw[1] || fw[2] || fw[3] || fw[4] || fw[5] || fw[6] || fw[7])  // ordered before the next launches
-        HIP_TRY(hipMemsetAsync((unsigned int*)c->flags.p + 1, 0, 7 * sizeof(unsigned int), c->stream));
+    c->n_qskip += fw[lgs::kFlagWordQSkip];
+    bool any = false;
+    for (int k = 1; k < lgs::kFlagWords; ++k) any |= fw[k] != 0;
+    if (any)  // ordered before the next launches
+        HIP_TRY(hipMemsetAsync((unsigned int*)c->flags.p + 1, 0, (lgs::kFlagWords - 1) * sizeof(unsigned int),
+                               c->stream));
     if (f & lgs::kFlagNonFinite)
         return fail(LGS_ERR_NONFINITE, "non-finite conditional mean (reference raises ValueError)");
     if (f & lgs::kFlagOverflow)
@@ -290,7 +297,7 @@ int finish(lgs_ctx* c, const unsigned int* fw_known = nullptr) {  // sync, fold 
 int finish_or_redo(lgs_ctx* c, bool oz_used, int& zb, bool& redo) {
     redo = false;
     HIP_TRY(hipStreamSynchronize(c->stream));
-    unsigned int fw[8];
+    unsigned int fw[lgs::kFlagWords];
     HIP_TRY(hipMemcpy(fw, c->flags.p, sizeof(fw), hipMemcpyDeviceToHost));
     if (!(fw[0] & lgs::kAbortMask)) return finish(c, fw);
     c->pending_i8.clear();
@@ -307,16 +314,16 @@ int finish_or_redo(lgs_ctx* c, bool oz_used, int& zb, bool& redo) {
     }
     if (fw[0] & lgs::kFlagCarry16) c->zint = 4;
     if (zb == 2) zb = c->zint;
-    HIP_TRY(hipMemsetAsync(c->flags.p, 0, 32, c->stream));
+    HIP_TRY(hipMemsetAsync(c->flags.p, 0, 4 * lgs::kFlagWords, c->stream));
     redo = true;
     return LGS_OK;
 }
 
 int reset_flags(lgs_ctx* c) {
-    int rc = c->flags.reserve(32);
+    int rc = c->flags.reserve(4 * lgs::kFlagWords);
     if (rc) return rc;
     c->resolved_seen = 0;
-    HIP_TRY(hipMemsetAsync(c->flags.p, 0, 32, c->stream));
+    HIP_TRY(hipMemsetAsync(c->flags.p, 0, 4 * lgs::kFlagWords, c->stream));
     return LGS_OK;
 }
 
@@ -451,6 +458,7 @@ int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
     Scope s(c, 1);
     HIP_TRY(lgs::launch::bz(b.Z, b.zb, b.ldz, b.sel, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
                             b.rstride, b.roff, c->stream));
+    if (b.VN) HIP_TRY(lgs::launch::vnorm2_rows(b.V, (int)c->d, b.n, b.rb, b.rstride, b.roff, b.VN, c->stream));
     return LGS_OK;
 }
 
@@ -460,25 +468,34 @@ int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
 // then a valid source of the digits for the columns that launch wrote).
 int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
            int64_t rb = 0, int64_t rstride = 0, int64_t roff = 0, const int64_t* sel = nullptr,
-           bool after_klein = false, const unsigned int* abort = nullptr) {
+           bool after_klein = false, const unsigned int* abort = nullptr, double* VN = nullptr) {
     if (!c->has_B) return fail(LGS_ERR_STATE, "lattice points need B (lgs_set_basis B != NULL)");
-    BzCall b{Z, zb, ldz, n, V, rb > 0 ? rb : n, rstride, roff, sel};
+    BzCall b{Z, zb, ldz, n, V, rb > 0 ? rb : n, rstride, roff, sel, VN};
     static const bool force64 = getenv("LGS_BZ_FP64") && atoi(getenv("LGS_BZ_FP64")) == 1;
     if (!c->has_Bi8 || force64) {
         Scope s(c, 1);
         HIP_TRY(lgs::launch::bz(b.Z, b.zb, b.ldz, b.sel, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
                                 b.rstride, b.roff, c->stream, abort));
+        if (VN) HIP_TRY(lgs::launch::vnorm2_rows(b.V, (int)c->d, b.n, b.rb, b.rstride, b.roff, VN, c->stream));
         return LGS_OK;
     }
     Scope s(c, 1);
     const int8_t* hi = c->Bd.as<int8_t>();
     const int8_t* lo = hi + (size_t)c->bd_rows * c->bd_cols;
+    double* VNP = nullptr;
+    if (VN) {
+        const int rc = c->VNP.reserve((size_t)2 * ((c->d + 127) / 128) * n * 8);
+        if (rc) return rc;
+        VNP = c->VNP.as<double>();
+    }
     HIP_TRY(lgs::launch::bz_i8(Z, zb, ldz, sel, c->kchunk.as<int>(), c->koff.as<int>(), hi, lo,
                                (int)c->bd_cols, (int)c->d, n, V, c->d, b.rb,
                                b.rstride, b.roff, c->flags.as<unsigned int>(),
                                after_klein && c->hist.Z == Z && Z ? c->H16.as<int16_t>() : nullptr, c->hist.lanes,
                                c->hist.cols, c->stream, abort, c->ZNZ.as<uint8_t>(),
-                               after_klein && c->hist.Z == Z && Z ? c->hist.clive : nullptr, c->hist.clive_ld));
+                               after_klein && c->hist.Z == Z && Z ? c->hist.clive : nullptr, c->hist.clive_ld,
+                               VNP));
+    if (VN) HIP_TRY(lgs::launch::vnorm2_reduce(VNP, (int)c->d, n, b.rb, b.rstride, b.roff, VN, c->stream, abort));
     c->pending_i8.push_back(b);
     return LGS_OK;
 }
@@ -1078,18 +1095,45 @@ int lgs_log_density(lgs_ctx* c, int64_t n, const void* z, double* out, uint32_t 
     return finish(c);
 }
 
+static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64_t first_step,
+                     int64_t n_steps, int32_t thin, void* z_state, double* logw_state, int32_t* state_init,
+                     int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
+                     double* logw_samples, uint8_t* accepted, double* vnorm2_samples, int64_t* zk_samples,
+                     int64_t zk_index, uint32_t flags);
+
 int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64_t first_step,
              int64_t n_steps, int32_t thin, void* z_state, double* logw_state, int32_t* state_init,
              int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
              uint32_t flags) {
-    return lgs_imhk_trace(c, seed, first_chain, nc, first_step, n_steps, thin, z_state, logw_state,
-                          state_init, accepts, z_samples, v_samples, moments, nullptr, nullptr, flags);
+    return imhk_impl(c, seed, first_chain, nc, first_step, n_steps, thin, z_state, logw_state, state_init,
+                     accepts, z_samples, v_samples, moments, nullptr, nullptr, nullptr, nullptr, 0, flags);
 }
 
 int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64_t first_step,
                    int64_t n_steps, int32_t thin, void* z_state, double* logw_state, int32_t* state_init,
                    int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
                    double* logw_samples, uint8_t* accepted, uint32_t flags) {
+    return imhk_impl(c, seed, first_chain, nc, first_step, n_steps, thin, z_state, logw_state, state_init,
+                     accepts, z_samples, v_samples, moments, logw_samples, accepted, nullptr, nullptr, 0, flags);
+}
+
+int lgs_imhk_ex(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64_t first_step,
+                int64_t n_steps, int32_t thin, void* z_state, double* logw_state, int32_t* state_init,
+                int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
+                const lgs_imhk_outputs* out, uint32_t flags) {
+    if (!out)
+        return imhk_impl(c, seed, first_chain, nc, first_step, n_steps, thin, z_state, logw_state, state_init,
+                         accepts, z_samples, v_samples, moments, nullptr, nullptr, nullptr, nullptr, 0, flags);
+    return imhk_impl(c, seed, first_chain, nc, first_step, n_steps, thin, z_state, logw_state, state_init,
+                     accepts, z_samples, v_samples, moments, out->logw_samples, out->accepted,
+                     out->vnorm2_samples, out->zk_samples, out->zk_index, flags);
+}
+
+static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64_t first_step,
+                     int64_t n_steps, int32_t thin, void* z_state, double* logw_state, int32_t* state_init,
+                     int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
+                     double* logw_samples, uint8_t* accepted, double* vnorm2_samples, int64_t* zk_samples,
+                     int64_t zk_index, uint32_t flags) {
     int rc = check_ctx(c);
     if (rc) return rc;
     if (nc < 0 || n_steps < 0 || thin < 1) return fail(LGS_ERR_INVALID, "bad nc/n_steps/thin");
@@ -1104,6 +1148,10 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
         return fail(LGS_ERR_INVALID, "v_samples needs LGS_DEVICE_PTRS (use lgs_lattice_points on z_samples)");
     if (z_samples && cm)
         return fail(LGS_ERR_INVALID, "z_samples is row-major (n_chains x n_keep x d) only");
+    if ((vnorm2_samples || zk_samples) && !dev)
+        return fail(LGS_ERR_INVALID, "vnorm2_samples / zk_samples need LGS_DEVICE_PTRS");
+    if (vnorm2_samples && !v_samples) return fail(LGS_ERR_INVALID, "vnorm2_samples needs v_samples");
+    if (zk_samples && (zk_index < 0 || zk_index >= c->d)) return fail(LGS_ERR_INVALID, "zk_index out of range");
     if (nc == 0) return LGS_OK;
     if (first_chain + (uint64_t)nc > (1ull << 32) || first_step + (uint64_t)n_steps > (1ull << 32))
         return fail(LGS_ERR_INVALID, "chain / step counters must stay below 2^32");
@@ -1240,7 +1288,7 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
         aa.LW = c->LW.as<double>();
         aa.lw_state = lws;
         aa.accepts = acc;
-        aa.sel = (z_samples || v_samples) && kb > 0 ? c->sel.as<int64_t>() : nullptr;
+        aa.sel = (z_samples || v_samples || zk_samples) && kb > 0 ? c->sel.as<int64_t>() : nullptr;
         aa.final_sel = c->fsel.as<int64_t>();
         aa.carry_col = carry ? npb : -1;
         aa.cnt = moments ? c->cnt.as<int32_t>() : nullptr;
@@ -1272,7 +1320,8 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
         }
         // The final-state gather rides on the moments pass unless a later step of this
         // block still reads the carried-in states (kept-state gather without carry columns).
-        const bool fuse_final = moments && !(z_samples && kb > 0 && !carry) && npb < ((int64_t)1 << 32);
+        const bool fuse_final = moments && !((z_samples || zk_samples) && kb > 0 && !carry) &&
+                                npb < ((int64_t)1 << 32);
         if (moments) {
             Scope s(c, 3);
             // carried-in states first: the fused pass overwrites z_state
@@ -1285,7 +1334,7 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
                                                ob, cm, nc, c->stream, fl, zflags ? c->ZNZ.as<uint8_t>() : nullptr,
                                                c->hist.lanes, (int)((16 - d % 16) % 16)));
         }
-        if ((z_samples || v_samples) && kb > 0) {
+        if ((z_samples || v_samples || zk_samples) && kb > 0) {
             // kept states q = chain*kb + k, gathered coordinate-major (d x nq); chain-major
             // proposal order makes this a near-contiguous copy (outputs only: an aborted
             // attempt's values are overwritten by the redo)
@@ -1293,9 +1342,13 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
             if (v_samples) {  // rows (chain, first_keep + k) of the n_chains x n_keep x d output,
                               // read straight from the proposal store through the selections
                 if ((rc = run_bz(c, c->Z.p, zb, ldzb, nq, v_samples, kb, n_keep, first_keep,
-                                 c->sel.as<int64_t>(), true, fl)))
+                                 c->sel.as<int64_t>(), true, fl, vnorm2_samples)))
                     return rc;
             }
+            if (zk_samples)
+                HIP_TRY(lgs::launch::coord_gather(c->Z.p, zb, ldzb, c->sel.as<int64_t>(), nq, kb, zs, ob, cm, nc,
+                                                  (int)d, (int)zk_index, zk_samples, kb, n_keep, first_keep,
+                                                  c->stream, fl));
             if (z_samples) {
                 if ((rc = c->stage_f.reserve((size_t)nq * d * ob))) return rc;
                 HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, ldzb, c->sel.as<int64_t>(), nq, kb, zs, ob, cm,
@@ -1388,12 +1441,13 @@ int lgs_timing_get(lgs_ctx* c, int kernel, double* ms, int64_t* n) {
 
 int lgs_counter(lgs_ctx* c, int which, int reset, uint64_t* value) {
     if (!c) return fail(LGS_ERR_INVALID, "null context");
-    if (which < LGS_COUNTER_RESOLVED || which > LGS_COUNTER_WL_MISMATCH)
-        return fail(LGS_ERR_INVALID, "counter id 0..3");
+    if (which < LGS_COUNTER_RESOLVED || which > LGS_COUNTER_QSKIP)
+        return fail(LGS_ERR_INVALID, "counter id 0..4");
     uint64_t& v = which == LGS_COUNTER_RESOLVED      ? c->n_resolved
                   : which == LGS_COUNTER_FALLBACK    ? c->n_fallback
                   : which == LGS_COUNTER_ACCEPT_RESOLVED ? c->n_accept_resolved
-                                                     : c->n_wl_mismatch;
+                  : which == LGS_COUNTER_WL_MISMATCH ? c->n_wl_mismatch
+                                                     : c->n_qskip;
     if (value) *value = v;
     if (reset) v = 0;
     return LGS_OK;
@@ -1570,6 +1624,15 @@ int lgs_gram(lgs_ctx* c, int64_t d, int64_t n, const void* x, int64_t ldx, const
             HIP_TRY(lgs::launch::gram_pack(Xin, xt, cm, ldx, (int)d, n, (const long long*)SH, Ph, Pl, ldp,
                                            c->flags.as<unsigned int>(), c->stream));
             HIP_TRY(lgs::launch::gram_planes(Ph, Pl, ldp, (int)d, G, S, c->stream, c->flags.as<unsigned int>()));
+            if (dev && gram_out && sum_out && cm && c->stream != c->own) {
+                // caller-owned device accumulators, coordinate-major input, on a stream the
+                // caller set (lgs_set_stream: it orders its own work after ours): the exact
+                // VALU replay is gated on the same flag, so nothing needs the host -- no
+                // synchronisation (the next call's flag reset is stream-ordered)
+                HIP_TRY(lgs::launch::gram(Xin, xt, ldx, (int)d, n, SH, G, S, c->stream,
+                                          c->flags.as<unsigned int>()));
+                return LGS_OK;
+            }
         }
         HIP_TRY(hipMemcpyAsync(&f, c->flags.p, sizeof(f), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));

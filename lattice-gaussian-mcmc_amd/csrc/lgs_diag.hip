@@ -376,7 +376,10 @@ template <typename ZT, typename AT>
 __global__ __launch_bounds__(256) void gram_val_kernel(const ZT* __restrict__ Z, int64_t ldz, int d,
                                                        int64_t n, int64_t kc, int nt,
                                                        const AT* __restrict__ shift, AT* __restrict__ G,
-                                                       AT* __restrict__ S) {
+                                                       AT* __restrict__ S, const unsigned int* gate) {
+    // gate (nullable): run only when the int8 packing flagged a value beyond two digits
+    // (the exact replay of gram_planes, decided on the device)
+    if (gate && !(*(const volatile unsigned int*)gate & kFlagI8Range)) return;
     constexpr int BT = 64, KS = 16;
     __shared__ AT As[KS][BT + 1], Bs[KS][BT + 1];
     const int tid = threadIdx.x;
@@ -688,17 +691,17 @@ int64_t gram_chunk(int64_t n, int nt) {
 }
 
 hipError_t gram(const void* Z, int xtype, int64_t ldz, int d, int64_t n, const void* shift, void* G,
-                void* S, hipStream_t st) {
+                void* S, hipStream_t st, const unsigned int* gate) {
     if (n <= 0 || d <= 0) return hipSuccess;
     const int nt = (d + 63) / 64;
     const int64_t kc = gram_chunk(n, nt);
     const dim3 grid((unsigned)(nt * (nt + 1) / 2), (unsigned)((n + kc - 1) / kc));
     if (xtype == 2)
-        hipLaunchKernelGGL((gram_val_kernel<int64_t, long long>), grid, dim3(256), 0, st, (const int64_t*)Z, ldz, d, n, kc, nt, (const long long*)shift, (long long*)G, (long long*)S);
+        hipLaunchKernelGGL((gram_val_kernel<int64_t, long long>), grid, dim3(256), 0, st, (const int64_t*)Z, ldz, d, n, kc, nt, (const long long*)shift, (long long*)G, (long long*)S, gate);
     else if (xtype == 1)
-        hipLaunchKernelGGL((gram_val_kernel<int32_t, long long>), grid, dim3(256), 0, st, (const int32_t*)Z, ldz, d, n, kc, nt, (const long long*)shift, (long long*)G, (long long*)S);
+        hipLaunchKernelGGL((gram_val_kernel<int32_t, long long>), grid, dim3(256), 0, st, (const int32_t*)Z, ldz, d, n, kc, nt, (const long long*)shift, (long long*)G, (long long*)S, gate);
     else
-        hipLaunchKernelGGL((gram_val_kernel<double, double>), grid, dim3(256), 0, st, (const double*)Z, ldz, d, n, kc, nt, (const double*)shift, (double*)G, (double*)S);
+        hipLaunchKernelGGL((gram_val_kernel<double, double>), grid, dim3(256), 0, st, (const double*)Z, ldz, d, n, kc, nt, (const double*)shift, (double*)G, (double*)S, gate);
     return hipGetLastError();
 }
 

@@ -151,6 +151,8 @@ struct KleinArgs {
 // Wang-Ling accept decisions (imhk_accept_kernel)
 constexpr int kFlagWordAcceptResolved = 6;  // decisions redone at reference-order weights
 constexpr int kFlagWordWLMismatch = 7;      // recomputed draws that did not reproduce the stored z (a bug)
+constexpr int kFlagWordQSkip = 8;           // (wave, panel) pairs of the q-panel skip (klein_mfma_kernel)
+constexpr int kFlagWords = 16;              // the flag buffer: 64 bytes
 
 struct AcceptArgs {
     int64_t nc;
@@ -218,7 +220,7 @@ hipError_t series_stats(const SeriesArgs& a, hipStream_t st);
 // ADDED to G / S; x coordinate-major (d x n, ld ldz).  VALU: exact int64 for
 // integer x (xtype 1 int32, 2 int64; shift int64), fp64 for xtype 0 (shift fp64).
 hipError_t gram(const void* Z, int xtype, int64_t ldz, int d, int64_t n, const void* shift, void* G,
-                void* S, hipStream_t st);
+                void* S, hipStream_t st, const unsigned int* gate = nullptr);
 // int8-digit path: pack y = x - shift into digit planes Ph / Pl ((d rounded up to
 // 128) rows x ldp bytes, ldp = n rounded up to 64; sets kFlagI8Range when some
 // |y| > 32639), then the MFMA Gram of the planes (upper block triangle + mirror:
@@ -288,7 +290,18 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
                  hipStream_t st, const unsigned int* abort = nullptr, const uint8_t* znz = nullptr,
-                 const unsigned int* clive = nullptr, int64_t clive_ld = 0);
+                 const unsigned int* clive = nullptr, int64_t clive_ld = 0, double* VNP = nullptr);
+// VNP (nullable, 2 ceil(d / 128) x n): per-(half coordinate tile, row) partial sums of ||v||^2
+// (bz_i8), summed per row into VN by vnorm2_reduce
+hipError_t vnorm2_reduce(const double* VNP, int d, int64_t n, int64_t rb, int64_t rstride, int64_t roff,
+                         double* VN, hipStream_t st, const unsigned int* abort = nullptr);
+// scalar functionals of kept states: coefficient k of selection q, and
+// ||v||^2 of the rows of V (row index (q / rb) * rstride + roff + q % rb in both)
+hipError_t coord_gather(const void* Z, int zb, int64_t ldz, const int64_t* sel, int64_t nq, int64_t q_per_chain,
+                        const void* zs, int ob, int zs_coord_major, int64_t nc, int d, int k, int64_t* out,
+                        int64_t rb, int64_t rstride, int64_t roff, hipStream_t st, const unsigned int* abort);
+hipError_t vnorm2_rows(const double* V, int d, int64_t n, int64_t rb, int64_t rstride, int64_t roff, double* VN,
+                       hipStream_t st);
 // ---- decoding
 // V (row-major n x d) = rows s: sum_c MT[c][r] X[c][s], X coordinate-major fp64 (fp64 MFMA)
 hipError_t gemm_f64(const double* X, int64_t ldx, const double* MT, int d, int64_t n, double* V,

@@ -1077,7 +1077,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
     // outside speculative sub-panels (+inf once a speculative coordinate is nonzero),
     // and the block's vote for skipping the current panel
     __shared__ double qzs[PB == 32 ? 256 : 1];
-    __shared__ int qskip_blk;
+    __shared__ int qskip_blk[2];  // (by panel parity: a wave may start the next panel before another
+                                  // has read this panel's vote when there is no block barrier between)
     if constexpr (PB == 32) {
         cert_lds[0][threadIdx.x] = 0.0;
 #ifdef LGS_NEAR_UNROLLED
@@ -1101,16 +1102,17 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
             // blocked mean (isr and ros are R_ii / sigma in two roundings).  Block-wide
             // (the far field stages the R-digit slab with block barriers).
             bool qtry = false;
-#ifndef LGS_NEAR_UNROLLED  // (that variant does not track ||z_W||)
+#if !defined(LGS_NEAR_UNROLLED) && !defined(LGS_NO_QSKIP_CODE)  // (that variant does not track ||z_W||)
             if constexpr (OZ && !WL)
                 qtry = a.qz2 != nullptr && p_hi >= 32 && ((const __attribute__((address_space(4))) double*)a.qz2)[pk] >= 0.0;
 #endif
             // records of coordinates r0 .. r0+31 (r0 = p_hi - 32; negative ones skipped)
-            if (qtry && threadIdx.x == 0) qskip_blk = 1;  // (every wave read the last panel's vote)
+            if (qtry && threadIdx.x == 0) qskip_blk[pk & 1] = 1;  // (read last at panel pk - 2: done)
             __syncthreads();
             if (qtry) {
                 const double q2 = ((const __attribute__((address_space(4))) double*)a.qz2)[pk];
-                if (__builtin_amdgcn_ballot_w64(active && !(qzs[threadIdx.x] <= q2)) != 0 && lane == 0) qskip_blk = 0;
+                if (__builtin_amdgcn_ballot_w64(active && !(qzs[threadIdx.x] <= q2)) != 0 && lane == 0)
+                    qskip_blk[pk & 1] = 0;
             }
             const int r0 = p_hi - 32;
             const double2* __restrict__ src = (const double2*)a.crec;
@@ -1119,7 +1121,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                 if (r0 * (kRecStride / 2) + e >= 0) dst[e] = src[(int64_t)r0 * (kRecStride / 2) + e];
             __syncthreads();
             if (!active) continue;
-            if (qtry && __builtin_amdgcn_readfirstlane(qskip_blk) != 0) {
+            if (qtry && __builtin_amdgcn_readfirstlane(qskip_blk[pk & 1]) != 0) {
+                if (lane == 0) atomicAdd(a.flags + kFlagWordQSkip, 1u);
 #pragma unroll
                 for (int s = 0; s < 32; ++s) {
                     Z[(size_t)(p_hi - 1 - s) * ldz + p] = (ZT)0;
@@ -1465,8 +1468,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         if constexpr (!WL) {  // sum z^2 of the sub-panel from its packed history (z + 128)
 #pragma unroll
                             for (int j = 0; j < 8; ++j) {
-                                const double zl = (double)((int)(hp[j] & 0xffffu) - 128);
-                                const double zh = (double)((int)(hp[j] >> 16) - 128);
+                                const double zl = (double)((int)(short)(hp[j] & 0xffffu) - 128);  // (int16: signed)
+                                const double zh = (double)((int)(short)(hp[j] >> 16) - 128);
                                 zsq = fma(zl, zl, zsq);
                                 zsq = fma(zh, zh, zsq);
                             }
@@ -1488,19 +1491,23 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     if constexpr (OZ) snz |= vo.nz != 0;
                     if (vo.z2 >= 0.0) zsq = vo.z2;
                 }
+#ifndef LGS_NO_QSKIP_CODE
                 if constexpr (OZ && !WL) {  // the q-panel skip's ||z_W||^2 (+inf: a speculative z != 0)
                     const bool spec_sp = rows16 == 16 &&
                                          __builtin_amdgcn_readfirstlane((int)((lds_cdptr)rec_lds)[(top - 1 - (p_hi - 32)) * kRecStride + kRecSpec]) == 1;
                     qzs[threadIdx.x] = spec_sp ? (zsq != 0.0 ? __builtin_inf() : qzs[threadIdx.x]) : qzs[threadIdx.x] + zsq;
                 }
+#endif
                 if constexpr (OZ) {
                     pnz |= snz;
                     if (a.znz) a.znz[(size_t)((top - 1 + a.h16_shift) >> 4) * a.h16_lanes + p] = snz ? 1 : 0;
                     // the wave's 64-coordinate chunk of these rows holds a nonzero (B z skips
                     // the others with one word per 32 chunks, not one flag load per chunk)
+#ifndef LGS_NO_CLIVE_K
                     if (a.clive && top >= 16 && __builtin_amdgcn_ballot_w64(snz) != 0 && lane == 0)
                         atomicOr(a.clive + (size_t)((top - 16) >> 11) * a.clive_ld + (p0 >> 6),
                                  1u << (((top - 16) >> 6) & 31));
+#endif
                 }
             };
             // one copy of the 16-step near field for both sub-panels (a second inlined
@@ -2373,7 +2380,8 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
                                                     const int16_t* __restrict__ h16, int64_t h16_lanes,
                                                     int64_t hcols, const unsigned int* abort,
                                                     const uint8_t* __restrict__ znz,
-                                                    const unsigned int* __restrict__ clive, int64_t clive_ld) {
+                                                    const unsigned int* __restrict__ clive, int64_t clive_ld,
+                                                    double* __restrict__ VNP) {
     if (aborted(abort)) return;  // (whole grid) the selections were not written
     constexpr int TA = LGS_BZ_TA;  // 32-sample MFMA tiles per wave
     constexpr int BM = 64 * TA, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
@@ -2550,6 +2558,43 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
 #pragma unroll
     for (int ta = 0; ta < TA; ++ta) {
     const int64_t qb = s0 + (wm * TA + ta) * 32;
+    if (VNP) {
+        // ||v||^2 of the tile's rows (a scalar functional of the kept states, SURVEY
+        // 8e): one partial sum per (row, 64-coordinate half tile), stored to its own
+        // slot VNP[(2 tx + wn) n + q] and summed per row by vnorm2_reduce_kernel (atomics
+        // on the 64 rows' few cache lines from 16 workgroups serialised: 0.5 ms per 2^20).
+        // Lane & 31 is the coordinate: the 16 rows' partial sums are reduced over the 32
+        // lanes by halving (16 shuffles instead of 80).  Integral v: exact in any order.
+        double vs[16];
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            vs[reg] = 0.0;
+#pragma unroll
+            for (int tn = 0; tn < 2; ++tn)
+                if (r0 + wn * 64 + tn * 32 + (lane & 31) < d) {
+                    const double v = fma((double)p1[ta][tn][reg], 65536.0, (double)p2[ta][tn][reg] * 256.0) +
+                                     (double)p3[ta][tn][reg];
+                    vs[reg] = fma(v, v, vs[reg]);
+                }
+        }
+        int ridx = 0;
+#pragma unroll
+        for (int half = 8; half >= 1; half >>= 1) {  // lane bit 16 -> 8 values, bit 8 -> 4, ...
+            const int bit = half * 2;
+            const bool up = (lane & bit) != 0;
+#pragma unroll
+            for (int j = 0; j < half; ++j) {
+                const double send = up ? vs[j] : vs[j + half];
+                const double keep = up ? vs[j + half] : vs[j];
+                vs[j] = keep + __shfl_xor(send, bit);
+            }
+            ridx += up ? half : 0;
+        }
+        const double tot = vs[0] + __shfl_xor(vs[0], 1);
+        const int row = (ridx & 3) + 8 * (ridx >> 2) + lrow;
+        const int64_t q = qb + row;
+        if (!(lane & 1) && q < n) VNP[(size_t)(2 * tx + wn) * n + q] = tot;
+    }
     const int64_t cb = qb / rb;
     const int64_t kb0 = qb - cb * rb;
     const int nrow = (int)min<int64_t>(n - qb, 32);  // valid rows of this tile
@@ -2598,6 +2643,59 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
     }
     }
     if (zmax > (ZT)32639 || zmin < (ZT)-32639) atomicOr(flags, kFlagI8Range);
+}
+
+// Coefficient k of each kept state (a scalar functional for lag sums):
+// out[(q / rb) * rstride + roff + q % rb] = z_k of selection q (sel[q] >= 0: column
+// of the proposal store, else the chain's carried-in state) -- gather_z for one row.
+template <typename ZT, typename OT>
+__global__ __launch_bounds__(256) void coord_gather_kernel(const ZT* __restrict__ Z, int64_t ldz,
+                                                           const int64_t* __restrict__ sel, int64_t nq,
+                                                           int64_t q_per_chain, const OT* __restrict__ zs,
+                                                           int zs_coord_major, int64_t nc, int d, int k,
+                                                           int64_t* __restrict__ out, int64_t rb, int64_t rstride,
+                                                           int64_t roff, const unsigned int* abort) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq || aborted(abort)) return;
+    const int64_t s = sel[q];
+    int64_t v;
+    if (s >= 0) {
+        v = (int64_t)Z[(size_t)k * ldz + s];
+    } else {
+        const int64_t c = q / q_per_chain;
+        v = (int64_t)(zs_coord_major ? zs[(size_t)k * nc + c] : zs[(size_t)c * d + k]);
+    }
+    out[(q / rb) * rstride + roff + q % rb] = v;
+}
+
+// ||v||^2 of rows q from bz_i8_kernel's partial sums VNP[k n + q], k < nparts (fixed
+// order), to VN[(q / rb) * rstride + roff + q % rb].
+__global__ __launch_bounds__(256) void vnorm2_reduce_kernel(const double* __restrict__ VNP, int nparts, int64_t n,
+                                                            int64_t rb, int64_t rstride, int64_t roff,
+                                                            double* __restrict__ VN, const unsigned int* abort) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n || aborted(abort)) return;
+    double s = 0.0;
+    for (int k = 0; k < nparts; ++k) s += VNP[(size_t)k * n + q];
+    VN[(q / rb) * rstride + roff + q % rb] = s;
+}
+
+// ||v||^2 of rows (q / rb) * rstride + roff + q % rb of V (ld d), one wave per row,
+// written (not added) to VN at the same row index: the fp64 B z paths (the int8 path
+// sums them in its epilogue).  Integral v: exact in any order.
+__global__ __launch_bounds__(256) void vnorm2_rows_kernel(const double* __restrict__ V, int d, int64_t n,
+                                                          int64_t rb, int64_t rstride, int64_t roff,
+                                                          double* __restrict__ VN) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (q >= n) return;
+    const int64_t row = (q / rb) * rstride + roff + q % rb;
+    const double* __restrict__ vr = V + (size_t)row * d;
+    double acc = 0.0;
+    for (int j = lane; j < d; j += 64) acc = fma(vr[j], vr[j], acc);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) VN[row] = acc;
 }
 
 // ============================================================ launchers
@@ -2736,6 +2834,30 @@ hipError_t gather_z(const void* Z, int zb, int64_t ldz, const int64_t* sel, int6
     return hipGetLastError();
 }
 
+hipError_t coord_gather(const void* Z, int zb, int64_t ldz, const int64_t* sel, int64_t nq, int64_t q_per_chain,
+                        const void* zs, int ob, int zs_coord_major, int64_t nc, int d, int k, int64_t* out,
+                        int64_t rb, int64_t rstride, int64_t roff, hipStream_t st, const unsigned int* abort) {
+    if (nq <= 0) return hipSuccess;
+    LGS_ZT(zb, ZT, LGS_ZT(ob, OT, hipLaunchKernelGGL((coord_gather_kernel<ZT, OT>), dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, (const ZT*)Z, ldz, sel, nq, q_per_chain, (const OT*)zs, zs_coord_major, nc, d, k, out, rb, rstride, roff, abort)));
+    return hipGetLastError();
+}
+
+hipError_t vnorm2_reduce(const double* VNP, int d, int64_t n, int64_t rb, int64_t rstride, int64_t roff,
+                         double* VN, hipStream_t st, const unsigned int* abort) {
+    if (n <= 0) return hipSuccess;
+    const int nparts = 2 * ((d + 127) / 128);
+    hipLaunchKernelGGL(vnorm2_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, VNP, nparts, n, rb,
+                       rstride, roff, VN, abort);
+    return hipGetLastError();
+}
+
+hipError_t vnorm2_rows(const double* V, int d, int64_t n, int64_t rb, int64_t rstride, int64_t roff, double* VN,
+                       hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(vnorm2_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, V, d, n, rb, rstride, roff, VN);
+    return hipGetLastError();
+}
+
 hipError_t uninit_scan(const int32_t* init, int64_t nc, unsigned int* any, hipStream_t st) {
     if (nc <= 0) return hipSuccess;
     const unsigned g = (unsigned)std::min<int64_t>((nc + 255) / 256, 1024);
@@ -2825,7 +2947,7 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
                  hipStream_t st, const unsigned int* abort, const uint8_t* znz, const unsigned int* clive,
-                 int64_t clive_ld) {
+                 int64_t clive_ld, double* VNP) {
     if (n <= 0) return hipSuccess;
     if (d % 16 != 0 || LGS_BZ_TA != 1 || d > kOzMaxD) h16 = nullptr;  // history blocks must align with the chunks
 #ifdef LGS_BZ_NO_ZNZ
@@ -2839,7 +2961,7 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
     const int tx = ((d + 127) / 128 + LGS_BZ_TXPER - 1) / LGS_BZ_TXPER;  // coordinate-tile groups
     const int64_t ty = (n + 64 * LGS_BZ_TA - 1) / (64 * LGS_BZ_TA);
     const dim3 grid((unsigned)(tx * ((ty + 7) / 8) * 8));  // whole rounds of 8 XCDs (extra tiles exit)
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort, znz, clive, clive_ld));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort, znz, clive, clive_ld, VNP));
     return hipGetLastError();
 }
 

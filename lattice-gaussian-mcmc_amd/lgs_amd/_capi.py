@@ -42,13 +42,21 @@ LGS_COUNTER_RESOLVED = 0
 LGS_COUNTER_FALLBACK = 1
 LGS_COUNTER_ACCEPT_RESOLVED = 2
 LGS_COUNTER_WL_MISMATCH = 3
+LGS_COUNTER_QSKIP = 4
 
 # every symbol include/lgs.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_destroy", "lgs_set_stream",
-           "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_imhk_trace", "lgs_lattice_points", "lgs_log_density", "lgs_sample_z", "lgs_timing_enable",
+           "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_imhk_trace", "lgs_imhk_ex", "lgs_lattice_points", "lgs_log_density", "lgs_sample_z", "lgs_timing_enable",
            "lgs_timing_get", "lgs_device_info", "lgs_series_stats", "lgs_gram",
            "lgs_jump_distance", "lgs_marginal_tvd", "lgs_column_range", "lgs_histogram", "lgs_set_decoder", "lgs_nearest_plane",
            "lgs_round_decode", "lgs_counter")
+
+
+class ImhkOutputs(ctypes.Structure):
+    """struct lgs_imhk_outputs (include/lgs.h)."""
+    _fields_ = [("logw_samples", ctypes.c_void_p), ("accepted", ctypes.c_void_p),
+                ("vnorm2_samples", ctypes.c_void_p), ("zk_samples", ctypes.c_void_p),
+                ("zk_index", ctypes.c_int64)]
 
 
 class LgsError(RuntimeError):
@@ -96,6 +104,9 @@ def load_library(path: str = LIB_PATH):
     L.lgs_imhk_trace.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint64,
                                  ctypes.c_int64, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                  _vp, _vp, ctypes.c_uint32]
+    L.lgs_imhk_ex.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint64,
+                              ctypes.c_int64, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                              ctypes.POINTER(ImhkOutputs), ctypes.c_uint32]
     L.lgs_lattice_points.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint32]
     L.lgs_log_density.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint32]
     L.lgs_sample_z.argtypes = [_vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int32, _vp, _vp,
@@ -246,10 +257,12 @@ class Context:
 
     def imhk(self, seed, first_chain, n_chains, first_step, n_steps, thin, z_state, logw_state,
              state_init, accepts, z_samples=None, v_samples=None, moments=None, flags=0,
-             logw_samples=None, accepted=None):
+             logw_samples=None, accepted=None, vnorm2_samples=None, zk_samples=None, zk_index=0):
         """lgs_imhk; with logw_samples (n_chains x n_steps/thin float64) or accepted
         (n_chains x n_steps uint8) lgs_imhk_trace, which also records each kept
-        state's log weight and each step's accept decision."""
+        state's log weight and each step's accept decision; with vnorm2_samples /
+        zk_samples (n_chains x n_steps/thin float64 / int64, device) lgs_imhk_ex, which
+        also gives ||v||^2 and coefficient zk_index of each kept state."""
         zt = "int64" if flags & LGS_Z64 else "int32"
         _check_bufs(flags, self.device, ((z_state, zt, "z_state"), (logw_state, "float64", "logw_state"),
                                          (state_init, "int32", "state_init"), (accepts, "int64", "accepts"),
@@ -259,7 +272,15 @@ class Context:
         args = (self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(first_chain), int(n_chains), int(first_step),
                 int(n_steps), int(thin), _ptr(z_state), _ptr(logw_state), _ptr(state_init), _ptr(accepts),
                 _ptr(z_samples), _ptr(v_samples), _ptr(moments))
-        if logw_samples is None and accepted is None:
+        if vnorm2_samples is not None or zk_samples is not None:
+            _check_bufs(flags, self.device, ((vnorm2_samples, "float64", "vnorm2_samples"),
+                                             (zk_samples, "int64", "zk_samples")))
+            def v(a):
+                q = _ptr(a)
+                return None if q is None else q.value
+            out = ImhkOutputs(v(logw_samples), v(accepted), v(vnorm2_samples), v(zk_samples), int(zk_index))
+            _check(_lib.lgs_imhk_ex(*args, ctypes.byref(out), int(flags)))
+        elif logw_samples is None and accepted is None:
             _check(_lib.lgs_imhk(*args, int(flags)))
         else:
             _check(_lib.lgs_imhk_trace(*args, _ptr(logw_samples), _ptr(accepted), int(flags)))

@@ -142,7 +142,9 @@ class LagSums:
         T = x.shape[1]
         xs = torch.cat([self.ring, x], 1)                      # (nc, L + T)
         win = xs.unfold(1, T, 1).flip(1)                       # win[:, k] = xs[:, L - k : L - k + T]
-        self.S += (win * x[:, None, :]).sum((0, 2))
+        # (the time axis first -- the contiguous one -- then the chains: one reduction
+        # over both axes runs as a strided reduction with a few dozen workgroups)
+        self.S += (win * x[:, None, :]).sum(2).sum(0)
         self.S1 += x.sum()
         self.ring.copy_(xs[:, T:] if T < L else x[:, T - L:])
 
@@ -173,7 +175,9 @@ class StreamingShard:
     ``advance(first_step, n_steps, acc, mom)`` advances this rank's chains by
     n_steps (adding accepted proposals per chain to ``acc`` and sum z / sum z^2 of
     the kept states to ``mom``) and returns their kept lattice points v
-    (n_chains x n_steps x d, fp64 tensor) or None.  The shard carries the lag-L
+    (n_chains x n_steps x d, fp64 tensor), or a dict with the two functionals
+    computed by the library ("zk": n_chains x n_steps int64, "vn2": ||v||^2 fp64 --
+    gpu_advance, lgs_imhk_ex), or None.  The shard carries the lag-L
     autocovariance sums of two scalar functionals of the first ``lag_chains``
     chains' kept states -- the coefficient z_k = round(<binv_row, v>) and
     1e-6 ||v||^2 -- across blocks, and ``reduce`` combines everything over the
@@ -236,6 +240,10 @@ class StreamingShard:
             self.n_gram += self.nc
 
     def _lag_device(self, v):
+        if isinstance(v, dict):  # the library's functionals of the kept states (no re-read of v)
+            self.lag_z.update_device(v["zk"][:self.lag_chains])
+            self.lag_v.update_device(v["vn2"][:self.lag_chains] * 1e-6)
+            return
         vs = v[:self.lag_chains]
         self.lag_z.update_device(self.t.round(vs @ self.binv).long())
         # ||v||^2 in one fused multiply-reduce pass over v (no v*v temporary); v is
@@ -245,7 +253,8 @@ class StreamingShard:
 
     def _lag_update(self, v):
         t = self.t
-        key = (v.data_ptr(), tuple(v.shape))
+        k0 = v["zk"] if isinstance(v, dict) else v
+        key = (k0.data_ptr(), tuple(k0.shape))
         if not self._graph_ok:
             self._lag_device(v)
         elif self._graph is not None and self._graph_key == key:
@@ -309,7 +318,8 @@ def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device,
           "lw": torch.zeros(n_chains, dtype=torch.float64, device=device),
           "init": torch.zeros(n_chains, dtype=torch.int32, device=device),
           "v": torch.empty((n_chains, block_steps, d), dtype=torch.float64, device=device)
-          if want_v and block_steps else None}
+          if want_v and block_steps else None,
+          "zk": None, "vn2": None}
     fl = flags | _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR
     lib_stream = torch.cuda.Stream(device=device)
     ctx.set_stream(lib_stream.cuda_stream)
@@ -324,11 +334,18 @@ def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device,
         v = st["v"]
         if want_v and (v is None or v.shape[1] != n_steps):
             v = st["v"] = torch.empty((n_chains, n_steps, d), dtype=torch.float64, device=device)
+        if want_v and (st["zk"] is None or st["zk"].shape[1] != n_steps):
+            st["zk"] = torch.empty((n_chains, n_steps), dtype=torch.int64, device=device)
+            st["vn2"] = torch.empty((n_chains, n_steps), dtype=torch.float64, device=device)
         _enter()
+        # the lag functionals z_{d-1} and ||v||^2 of every kept state come from the
+        # library (coefficient store / B z epilogue), not from re-reading v
         ctx.imhk(seed, first_chain, n_chains, first_step, n_steps, 1, st["z"], st["lw"], st["init"], acc,
-                 v_samples=v if want_v else None, moments=mom, flags=fl)
+                 v_samples=v if want_v else None, moments=mom, flags=fl,
+                 vnorm2_samples=st["vn2"] if want_v else None, zk_samples=st["zk"] if want_v else None,
+                 zk_index=d - 1)
         _leave()
-        return v if want_v else None
+        return {"v": v, "zk": st["zk"], "vn2": st["vn2"]} if want_v else None
 
     def gram(G, S):
         _enter()

@@ -171,12 +171,21 @@ def test_q_panel_skip_equals_full_computation(capi, oracle, cfg, center_scale, m
         z = torch.empty((d, n), dtype=torch.int32, device="cuda")
         lw = torch.empty(n, dtype=torch.float64, device="cuda")
         ctx.timing_enable(True)
+        ctx.counter(capi.LGS_COUNTER_QSKIP, reset=True)
         ctx.klein(17, 3 << 20, n, z, None, lw, capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR)
         ms, _ = ctx.timing_get(capi.KERNEL_KLEIN)
-        out[skip] = (z, lw, ms)
+        out[skip] = (z, lw, ms, ctx.counter(capi.LGS_COUNTER_QSKIP))
     ctx.klein(17, 3 << 20, n, out["1"][0], None, None, capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR | capi.LGS_EXACT_ORDER)
     torch.cuda.synchronize()
-    print(f"{cfg} center {center_scale}: skip {out['0'][2]:.3f} ms, no skip {out['1'][2]:.3f} ms")
+    qs = out["0"][3]
+    print(f"{cfg} center {center_scale}: skip {out['0'][2]:.3f} ms ({qs} wave-panels skipped), "
+          f"no skip {out['1'][2]:.3f} ms")
+    assert out["1"][3] == 0
+    nq = (sigma / np.diag(R) < 4.0).sum() // 32  # the q-panels
+    if center_scale == 0.0:
+        assert qs == nq * n // 64  # every q-panel of every wave
+    else:
+        assert qs == 0
     assert torch.equal(out["0"][0], out["1"][0])  # skipped panels: the same z as computed ones
     rel = float(((out["0"][1] - out["1"][1]).abs() / out["1"][1].abs().clamp_min(1.0)).max())
     assert rel < 1e-12, rel

@@ -93,3 +93,37 @@ def test_gpu_advance_streams_match_synchronized_run():
         for x, y in zip(xa, xb):
             assert np.array_equal(x, y), k
     assert 0 < int(a["accepts"][0]) < 2048 * 64
+
+
+@pytest.mark.parametrize("cfg", ["C3_ntru512", "C2_qary128"])
+def test_imhk_ex_functionals_equal_recomputation(cfg):
+    """lgs_imhk_ex's per-kept-state functionals -- ||v||^2 summed in the B z epilogue
+    and coefficient d-1 gathered from the proposal store -- equal the same quantities
+    recomputed from the kept lattice points / coefficients it also returns."""
+    import torch
+    from lgs_amd import _capi
+    from lgs_amd.lattices import build_config
+    import lgs_oracle
+    lat, sigma = build_config(cfg)
+    B = lat.basis
+    R, cp = lgs_oracle.qr_prepare(B)
+    d = B.shape[0]
+    ctx = _capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    nc, T = 512, 8
+    dev = "cuda:0"
+    z = torch.zeros((nc, d), dtype=torch.int32, device=dev)
+    lw = torch.zeros(nc, dtype=torch.float64, device=dev)
+    init = torch.zeros(nc, dtype=torch.int32, device=dev)
+    acc = torch.zeros(nc, dtype=torch.int64, device=dev)
+    for wl in (0, _capi.LGS_WANG_LING):  # (Wang-Ling: rejections keep carried-in states)
+        zs = torch.empty((nc, T, d), dtype=torch.int32, device=dev)
+        vs = torch.empty((nc, T, d), dtype=torch.float64, device=dev)
+        vn2 = torch.full((nc, T), -1.0, dtype=torch.float64, device=dev)
+        zk = torch.full((nc, T), -7, dtype=torch.int64, device=dev)
+        ctx.imhk(3, 0, nc, 1 + 2 * T * (wl != 0), T, 1, z, lw, init, acc, z_samples=zs, v_samples=vs,
+                 flags=_capi.LGS_DEVICE_PTRS | wl, vnorm2_samples=vn2, zk_samples=zk, zk_index=d - 1)
+        torch.cuda.synchronize()
+        assert torch.equal(vn2, (vs * vs).sum(-1))
+        assert torch.equal(zk, zs[:, :, d - 1].long())
+        assert torch.equal(vs, zs.double() @ torch.as_tensor(B, device=dev).T)
