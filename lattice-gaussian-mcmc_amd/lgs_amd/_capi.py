@@ -104,9 +104,10 @@ def load_library(path: str = LIB_PATH):
     L.lgs_imhk_trace.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint64,
                                  ctypes.c_int64, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                  _vp, _vp, ctypes.c_uint32]
-    L.lgs_imhk_ex.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint64,
-                              ctypes.c_int64, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                              ctypes.POINTER(ImhkOutputs), ctypes.c_uint32]
+    if hasattr(L, "lgs_imhk_ex"):  # (round 4; older builds, e.g. A/B baselines, lack it)
+        L.lgs_imhk_ex.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint64,
+                                  ctypes.c_int64, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  ctypes.POINTER(ImhkOutputs), ctypes.c_uint32]
     L.lgs_lattice_points.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint32]
     L.lgs_log_density.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint32]
     L.lgs_sample_z.argtypes = [_vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int32, _vp, _vp,

@@ -183,7 +183,9 @@ def test_q_panel_skip_equals_full_computation(capi, oracle, cfg, center_scale, m
     assert out["1"][3] == 0
     nq = (sigma / np.diag(R) < 4.0).sum() // 32  # the q-panels
     if center_scale == 0.0:
-        assert qs == nq * n // 64  # every q-panel of every wave
+        # (nearly) every q-panel of every wave: a block votes as one, and a block with a
+        # sample whose ||z_W|| exceeds a panel's bound computes that panel
+        assert 0.95 * (nq * n // 64) <= qs <= nq * n // 64
     else:
         assert qs == 0
     assert torch.equal(out["0"][0], out["1"][0])  # skipped panels: the same z as computed ones
