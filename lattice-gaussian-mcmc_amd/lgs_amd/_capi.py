@@ -129,7 +129,7 @@ def load_library(path: str = LIB_PATH):
     L.lgs_nearest_plane.argtypes = [_vp, _i64, _vp, _vp, _vp, ctypes.c_uint32]
     L.lgs_round_decode.argtypes = [_vp, _i64, _vp, _vp, _vp, ctypes.c_uint32]
     for name in EXPORTS:
-        if name not in ("lgs_version", "lgs_last_error"):
+        if name not in ("lgs_version", "lgs_last_error") and hasattr(L, name):
             getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
