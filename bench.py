@@ -210,7 +210,8 @@ def main():
     # the timed path is lgs_amd.distributed's StreamingShard: one lgs_imhk call per
     # bench step, lag sums on the device, one all-reduce (tests/test_distributed.py
     # drives the same class with the oracle over gloo, world 2)
-    advance = D.gpu_advance(ctx, seed, first_chain, nc, d, dev, flags=flags, block_steps=T, want_v=not args.no_v)
+    advance = D.gpu_advance(ctx, seed, first_chain, nc, d, dev, flags=flags, block_steps=T, want_v=not args.no_v,
+                            fn_chains=ACF_CHAINS)
     shard = D.StreamingShard(advance, nc, d, binv_row=binv_k, device=dev, lag_chains=ACF_CHAINS, lags=ACF_LAGS,
                              gram_every=args.gram_every)
     z_state = advance.state["z"]

@@ -79,7 +79,8 @@ struct BzCall {  // an int8-digit B z launch, replayed in fp64 if a digit overfl
     double* V;
     int64_t rb, rstride, roff;
     const int64_t* sel;  // nullable: sample s reads column sel[s] of Z
-    double* VN;          // nullable: ||v||^2 of each row (same row index, ld 1)
+    double* VN;          // nullable: ||v||^2 of rows q < vn_n (same row index, ld 1)
+    int64_t vn_n;
 };
 
 }  // namespace
@@ -120,6 +121,7 @@ struct lgs_ctx {
     DevBuf ZNZ;                   // per history block and lane: any nonzero z (B z's chunk skipping)
     DevBuf CLIVE;                 // per wave and 64-coordinate chunk: any nonzero z (bits; B z)
     DevBuf VNP;                   // B z's per-tile partial sums of ||v||^2 (lgs_imhk_ex vnorm2_samples)
+    DevBuf LAGP;                  // lag-sum partials per (lag, chain) (lgs_imhk_ex lag_L)
     // the last Klein launch's history, valid for columns [0, cols) of the store Z it
     // wrote (B z reads its digits from there); reset by every Klein launch
     struct {
@@ -458,7 +460,7 @@ int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
     Scope s(c, 1);
     HIP_TRY(lgs::launch::bz(b.Z, b.zb, b.ldz, b.sel, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
                             b.rstride, b.roff, c->stream));
-    if (b.VN) HIP_TRY(lgs::launch::vnorm2_rows(b.V, (int)c->d, b.n, b.rb, b.rstride, b.roff, b.VN, c->stream));
+    if (b.VN) HIP_TRY(lgs::launch::vnorm2_rows(b.V, (int)c->d, b.vn_n, b.rb, b.rstride, b.roff, b.VN, c->stream));
     return LGS_OK;
 }
 
@@ -468,15 +470,18 @@ int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
 // then a valid source of the digits for the columns that launch wrote).
 int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
            int64_t rb = 0, int64_t rstride = 0, int64_t roff = 0, const int64_t* sel = nullptr,
-           bool after_klein = false, const unsigned int* abort = nullptr, double* VN = nullptr) {
+           bool after_klein = false, const unsigned int* abort = nullptr, double* VN = nullptr,
+           int64_t vn_n = -1) {
     if (!c->has_B) return fail(LGS_ERR_STATE, "lattice points need B (lgs_set_basis B != NULL)");
-    BzCall b{Z, zb, ldz, n, V, rb > 0 ? rb : n, rstride, roff, sel, VN};
+    if (vn_n < 0 || vn_n > n) vn_n = n;  // ||v||^2 of the leading vn_n rows only
+    if (vn_n == 0) VN = nullptr;
+    BzCall b{Z, zb, ldz, n, V, rb > 0 ? rb : n, rstride, roff, sel, VN, vn_n};
     static const bool force64 = getenv("LGS_BZ_FP64") && atoi(getenv("LGS_BZ_FP64")) == 1;
     if (!c->has_Bi8 || force64) {
         Scope s(c, 1);
         HIP_TRY(lgs::launch::bz(b.Z, b.zb, b.ldz, b.sel, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
                                 b.rstride, b.roff, c->stream, abort));
-        if (VN) HIP_TRY(lgs::launch::vnorm2_rows(b.V, (int)c->d, b.n, b.rb, b.rstride, b.roff, VN, c->stream));
+        if (VN) HIP_TRY(lgs::launch::vnorm2_rows(b.V, (int)c->d, vn_n, b.rb, b.rstride, b.roff, VN, c->stream));
         return LGS_OK;
     }
     Scope s(c, 1);
@@ -484,7 +489,7 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
     const int8_t* lo = hi + (size_t)c->bd_rows * c->bd_cols;
     double* VNP = nullptr;
     if (VN) {
-        const int rc = c->VNP.reserve((size_t)2 * ((c->d + 127) / 128) * n * 8);
+        const int rc = c->VNP.reserve((size_t)2 * ((c->d + 127) / 128) * vn_n * 8);
         if (rc) return rc;
         VNP = c->VNP.as<double>();
     }
@@ -494,8 +499,8 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
                                after_klein && c->hist.Z == Z && Z ? c->H16.as<int16_t>() : nullptr, c->hist.lanes,
                                c->hist.cols, c->stream, abort, c->ZNZ.as<uint8_t>(),
                                after_klein && c->hist.Z == Z && Z ? c->hist.clive : nullptr, c->hist.clive_ld,
-                               VNP));
-    if (VN) HIP_TRY(lgs::launch::vnorm2_reduce(VNP, (int)c->d, n, b.rb, b.rstride, b.roff, VN, c->stream, abort));
+                               VNP, vn_n));
+    if (VN) HIP_TRY(lgs::launch::vnorm2_reduce(VNP, (int)c->d, vn_n, b.rb, b.rstride, b.roff, VN, c->stream, abort));
     c->pending_i8.push_back(b);
     return LGS_OK;
 }
@@ -1099,14 +1104,14 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
                      int64_t n_steps, int32_t thin, void* z_state, double* logw_state, int32_t* state_init,
                      int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
                      double* logw_samples, uint8_t* accepted, double* vnorm2_samples, int64_t* zk_samples,
-                     int64_t zk_index, uint32_t flags);
+                     int64_t zk_index, int64_t fn_chains, const lgs_imhk_outputs* lag, uint32_t flags);
 
 int lgs_imhk(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64_t first_step,
              int64_t n_steps, int32_t thin, void* z_state, double* logw_state, int32_t* state_init,
              int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
              uint32_t flags) {
     return imhk_impl(c, seed, first_chain, nc, first_step, n_steps, thin, z_state, logw_state, state_init,
-                     accepts, z_samples, v_samples, moments, nullptr, nullptr, nullptr, nullptr, 0, flags);
+                     accepts, z_samples, v_samples, moments, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, flags);
 }
 
 int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64_t first_step,
@@ -1114,7 +1119,7 @@ int lgs_imhk_trace(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, 
                    int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
                    double* logw_samples, uint8_t* accepted, uint32_t flags) {
     return imhk_impl(c, seed, first_chain, nc, first_step, n_steps, thin, z_state, logw_state, state_init,
-                     accepts, z_samples, v_samples, moments, logw_samples, accepted, nullptr, nullptr, 0, flags);
+                     accepts, z_samples, v_samples, moments, logw_samples, accepted, nullptr, nullptr, 0, 0, nullptr, flags);
 }
 
 int lgs_imhk_ex(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64_t first_step,
@@ -1123,17 +1128,18 @@ int lgs_imhk_ex(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uin
                 const lgs_imhk_outputs* out, uint32_t flags) {
     if (!out)
         return imhk_impl(c, seed, first_chain, nc, first_step, n_steps, thin, z_state, logw_state, state_init,
-                         accepts, z_samples, v_samples, moments, nullptr, nullptr, nullptr, nullptr, 0, flags);
+                         accepts, z_samples, v_samples, moments, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, flags);
     return imhk_impl(c, seed, first_chain, nc, first_step, n_steps, thin, z_state, logw_state, state_init,
                      accepts, z_samples, v_samples, moments, out->logw_samples, out->accepted,
-                     out->vnorm2_samples, out->zk_samples, out->zk_index, flags);
+                     out->vnorm2_samples, out->zk_samples, out->zk_index, out->fn_chains,
+                     out->lag_L > 0 ? out : nullptr, flags);
 }
 
 static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc, uint64_t first_step,
                      int64_t n_steps, int32_t thin, void* z_state, double* logw_state, int32_t* state_init,
                      int64_t* accepts, void* z_samples, double* v_samples, int64_t* moments,
                      double* logw_samples, uint8_t* accepted, double* vnorm2_samples, int64_t* zk_samples,
-                     int64_t zk_index, uint32_t flags) {
+                     int64_t zk_index, int64_t fn_chains, const lgs_imhk_outputs* lag, uint32_t flags) {
     int rc = check_ctx(c);
     if (rc) return rc;
     if (nc < 0 || n_steps < 0 || thin < 1) return fail(LGS_ERR_INVALID, "bad nc/n_steps/thin");
@@ -1152,6 +1158,14 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
         return fail(LGS_ERR_INVALID, "vnorm2_samples / zk_samples need LGS_DEVICE_PTRS");
     if (vnorm2_samples && !v_samples) return fail(LGS_ERR_INVALID, "vnorm2_samples needs v_samples");
     if (zk_samples && (zk_index < 0 || zk_index >= c->d)) return fail(LGS_ERR_INVALID, "zk_index out of range");
+    if (fn_chains < 0 || fn_chains > nc) return fail(LGS_ERR_INVALID, "fn_chains must be in [0, n_chains]");
+    if (fn_chains == 0) fn_chains = nc;  // the functionals of every chain's kept states
+    if (lag) {
+        if (lag->lag_L > (1 << 20)) return fail(LGS_ERR_INVALID, "lag_L too large");
+        if ((lag->lag_z_sums && (!zk_samples || !lag->lag_z_ring)) ||
+            (lag->lag_v_sums && (!vnorm2_samples || !lag->lag_v_ring)))
+            return fail(LGS_ERR_INVALID, "lag sums need their series (zk_samples / vnorm2_samples) and ring");
+    }
     if (nc == 0) return LGS_OK;
     if (first_chain + (uint64_t)nc > (1ull << 32) || first_step + (uint64_t)n_steps > (1ull << 32))
         return fail(LGS_ERR_INVALID, "chain / step counters must stay below 2^32");
@@ -1342,13 +1356,24 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             if (v_samples) {  // rows (chain, first_keep + k) of the n_chains x n_keep x d output,
                               // read straight from the proposal store through the selections
                 if ((rc = run_bz(c, c->Z.p, zb, ldzb, nq, v_samples, kb, n_keep, first_keep,
-                                 c->sel.as<int64_t>(), true, fl, vnorm2_samples)))
+                                 c->sel.as<int64_t>(), true, fl, vnorm2_samples, fn_chains * kb)))
                     return rc;
             }
-            if (zk_samples)
-                HIP_TRY(lgs::launch::coord_gather(c->Z.p, zb, ldzb, c->sel.as<int64_t>(), nq, kb, zs, ob, cm, nc,
+            if (zk_samples)  // (the leading fn_chains chains' kept states: q < fn_chains * kb)
+                HIP_TRY(lgs::launch::coord_gather(c->Z.p, zb, ldzb, c->sel.as<int64_t>(), fn_chains * kb, kb, zs, ob, cm, nc,
                                                   (int)d, (int)zk_index, zk_samples, kb, n_keep, first_keep,
                                                   c->stream, fl));
+            if (lag) {  // this block's kb new values of each chain's series, in time order
+                const int L = (int)lag->lag_L;
+                if ((rc = c->LAGP.reserve((size_t)(L + 2) * fn_chains * 8))) return rc;
+                if (lag->lag_z_sums)
+                    HIP_TRY(lgs::launch::lag_update(zk_samples + first_keep, 0, n_keep, fn_chains, kb, L, 1.0,
+                                                    lag->lag_z_ring, lag->lag_z_sums, c->LAGP.p, c->stream, fl));
+                if (lag->lag_v_sums)
+                    HIP_TRY(lgs::launch::lag_update(vnorm2_samples + first_keep, 1, n_keep, fn_chains, kb, L,
+                                                    lag->lag_v_scale, lag->lag_v_ring, lag->lag_v_sums, c->LAGP.p,
+                                                    c->stream, fl));
+            }
             if (z_samples) {
                 if ((rc = c->stage_f.reserve((size_t)nq * d * ob))) return rc;
                 HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, ldzb, c->sel.as<int64_t>(), nq, kb, zs, ob, cm,

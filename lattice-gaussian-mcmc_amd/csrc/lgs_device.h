@@ -981,7 +981,12 @@ __device__ __forceinline__ double sample_z_capped(double mu, double u, const QHe
     {
         const double xs = fma((xg - m) * (-1.0 / 24.0), is * is, xg - 0.5);
         const double fl = floor(xs);
-        const double tol = fma(2.94e-8, fabs(xg - m), CERT ? fma(4.5, dmu, 1e-8) : 1e-8);  // (plain: dmu < 0)
+        // (the constant through a scalar register: hoisted into a VGPR pair out of the
+        // near-field loop, the compiler spilled it, and its reload's vmcnt(0) waited for
+        // every coordinate's stores)
+        double t0 = 1e-8;
+        asm volatile("" : "+s"(t0));
+        const double tol = fma(2.94e-8, fabs(xg - m), CERT ? fma(4.5, dmu, t0) : t0);  // (plain: dmu < 0)
 #ifdef LGS_DIAG_CAPQ  // diagnostic builds only: why the quantile decision falls through
         {
             const bool ca = !(xs - fl > tol && fl + 1.0 - xs > tol), cb = !(fl >= -501.0 && fl <= 499.0),

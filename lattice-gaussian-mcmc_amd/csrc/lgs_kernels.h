@@ -290,13 +290,19 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
                  hipStream_t st, const unsigned int* abort = nullptr, const uint8_t* znz = nullptr,
-                 const unsigned int* clive = nullptr, int64_t clive_ld = 0, double* VNP = nullptr);
-// VNP (nullable, 2 ceil(d / 128) x n): per-(half coordinate tile, row) partial sums of ||v||^2
-// (bz_i8), summed per row into VN by vnorm2_reduce
+                 const unsigned int* clive = nullptr, int64_t clive_ld = 0, double* VNP = nullptr,
+                 int64_t vn_n = 0);
+// VNP (nullable, 2 ceil(d / 128) x vn_n): per-(half coordinate tile, row) partial sums of
+// ||v||^2 of rows q < vn_n (bz_i8), summed per row into VN by vnorm2_reduce (n = vn_n)
 hipError_t vnorm2_reduce(const double* VNP, int d, int64_t n, int64_t rb, int64_t rstride, int64_t roff,
                          double* VN, hipStream_t st, const unsigned int* abort = nullptr);
 // scalar functionals of kept states: coefficient k of selection q, and
 // ||v||^2 of the rows of V (row index (q / rb) * rstride + roff + q % rb in both)
+// lag-L sums of nc per-chain series (int64, or fp64 scaled by scale), T new values each
+// (row stride ldx), continued through ring (nc x L); sums (L + 2: lags 0..L, then sum x)
+// added to; P scratch of (L + 2) nc values
+hipError_t lag_update(const void* X, int is_f64, int64_t ldx, int64_t nc, int64_t Tn, int L, double scale,
+                      void* ring, void* sums, void* P, hipStream_t st, const unsigned int* abort = nullptr);
 hipError_t coord_gather(const void* Z, int zb, int64_t ldz, const int64_t* sel, int64_t nq, int64_t q_per_chain,
                         const void* zs, int ob, int zs_coord_major, int64_t nc, int d, int k, int64_t* out,
                         int64_t rb, int64_t rstride, int64_t roff, hipStream_t st, const unsigned int* abort);

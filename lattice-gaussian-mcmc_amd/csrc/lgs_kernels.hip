@@ -1070,8 +1070,6 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
     // coordinate at this kernel's register pressure)
 #ifdef LGS_NEAR_UNROLLED
     __shared__ int cert_fl[PB == 32 ? 256 : 1];
-#else
-    __shared__ int cert_fl[1];
 #endif
     // q-panel skip (reference mode, a.qz2): per lane sum z_j^2 over the coordinates
     // outside speculative sub-panels (+inf once a speculative coordinate is nonzero),
@@ -1405,7 +1403,6 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                 int flm = 0;
                 bool snz = false;  // (OZ) a nonzero z in this sub-panel, this lane
                 double zsq = 0.0;  // (q-panel skip) sum z^2 of this sub-panel, this lane
-                typedef double d2v __attribute__((ext_vector_type(2)));
 #ifndef LGS_NEAR_UNROLL  // coordinates per loop iteration (the running sums shift by one per step)
 #define LGS_NEAR_UNROLL 1
 #endif
@@ -1455,7 +1452,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         }
                         snz |= zi != 0.0;
                     }
-                    z1e += fabs(zi);
+                    // sum |z|: only the sub-panel's end reads it (the certificate's per-coordinate
+                    // bound uses the cap), so a whole 16-row sub-panel takes it from the packed
+                    // history below (exact: integers) -- kept in the loop, the compiler spilled
+                    // it and its reload's vmcnt(0) waited for every coordinate's stores
+                    if (!hblock) z1e += fabs(zi);
 #pragma unroll
                     for (int k = 14; k >= 0; --k) acc[k + 1] = fma(rr[kRecRs + 14 - k], zi, acc[k]);
                     acc[0] = 0.0;
@@ -1465,11 +1466,14 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         v4u_t* hp4 = (v4u_t*)(a.h16 + ((size_t)((top - 16 + a.h16_shift) >> 4) * a.h16_lanes + p) * 16);
                         hp4[0] = (v4u_t){hp[0], hp[1], hp[2], hp[3]};
                         hp4[1] = (v4u_t){hp[4], hp[5], hp[6], hp[7]};
-                        if constexpr (!WL) {  // sum z^2 of the sub-panel from its packed history (z + 128)
+                        // sum |z| (and, reference mode, z^2) of the sub-panel from its packed
+                        // history (z + 128; int16: signed)
 #pragma unroll
-                            for (int j = 0; j < 8; ++j) {
-                                const double zl = (double)((int)(short)(hp[j] & 0xffffu) - 128);  // (int16: signed)
-                                const double zh = (double)((int)(short)(hp[j] >> 16) - 128);
+                        for (int j = 0; j < 8; ++j) {
+                            const double zl = (double)((int)(short)(hp[j] & 0xffffu) - 128);
+                            const double zh = (double)((int)(short)(hp[j] >> 16) - 128);
+                            z1e += fabs(zl) + fabs(zh);
+                            if constexpr (!WL) {
                                 zsq = fma(zl, zl, zsq);
                                 zsq = fma(zh, zh, zsq);
                             }
@@ -2381,7 +2385,7 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
                                                     int64_t hcols, const unsigned int* abort,
                                                     const uint8_t* __restrict__ znz,
                                                     const unsigned int* __restrict__ clive, int64_t clive_ld,
-                                                    double* __restrict__ VNP) {
+                                                    double* __restrict__ VNP, int64_t vn_n) {
     if (aborted(abort)) return;  // (whole grid) the selections were not written
     constexpr int TA = LGS_BZ_TA;  // 32-sample MFMA tiles per wave
     constexpr int BM = 64 * TA, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
@@ -2558,11 +2562,13 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
 #pragma unroll
     for (int ta = 0; ta < TA; ++ta) {
     const int64_t qb = s0 + (wm * TA + ta) * 32;
-    if (VNP) {
+    if (VNP && qb < vn_n) {
         // ||v||^2 of the tile's rows (a scalar functional of the kept states, SURVEY
         // 8e): one partial sum per (row, 64-coordinate half tile), stored to its own
-        // slot VNP[(2 tx + wn) n + q] and summed per row by vnorm2_reduce_kernel (atomics
+        // slot VNP[(2 tx + wn) vn_n + q] and summed per row by vnorm2_reduce_kernel (atomics
         // on the 64 rows' few cache lines from 16 workgroups serialised: 0.5 ms per 2^20).
+        // Only the rows q < vn_n (the leading chains a lag series follows): computed for
+        // every row this epilogue cost 0.94 ms per 2^20 (bz 1.70 -> 2.65 ms).
         // Lane & 31 is the coordinate: the 16 rows' partial sums are reduced over the 32
         // lanes by halving (16 shuffles instead of 80).  Integral v: exact in any order.
         double vs[16];
@@ -2593,7 +2599,7 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
         const double tot = vs[0] + __shfl_xor(vs[0], 1);
         const int row = (ridx & 3) + 8 * (ridx >> 2) + lrow;
         const int64_t q = qb + row;
-        if (!(lane & 1) && q < n) VNP[(size_t)(2 * tx + wn) * n + q] = tot;
+        if (!(lane & 1) && q < vn_n) VNP[(size_t)(2 * tx + wn) * vn_n + q] = tot;
     }
     const int64_t cb = qb / rb;
     const int64_t kb0 = qb - cb * rb;
@@ -2678,6 +2684,69 @@ __global__ __launch_bounds__(256) void vnorm2_reduce_kernel(const double* __rest
     double s = 0.0;
     for (int k = 0; k < nparts; ++k) s += VNP[(size_t)k * n + q];
     VN[(q / rb) * rstride + roff + q % rb] = s;
+}
+
+// Lag-L sums of per-chain scalar series continued across calls (the
+// StreamingShard's LagSums, lgs_amd/distributed.py): for chains c < nc, the new values
+// x[c][t] = scale * X[c ldx + t] (t < T; int64 series unscaled) after the ring's last L
+// values r[c][0..L-1]: P[k nc + c] = sum_t x_t x_{t-k} for k <= L (values before the
+// ring's start are 0) and P[(L + 1) nc + c] = sum_t x_t, one thread per (k, chain);
+// lag_finish_kernel adds the partials to sums[k] in a fixed order and moves each ring
+// to the chain's last L values.  int64 series: exact; fp64: reproducible.
+template <typename T>
+__device__ __forceinline__ T lag_val(const T* __restrict__ rr, const T* __restrict__ xr, int L, int64_t u,
+                                     double scale) {
+    if (u < L) return rr[u];  // u in [0, L + T): the ring, then the new values
+    if constexpr (std::is_floating_point<T>::value) return xr[u - L] * scale;
+    return xr[u - L];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void lag_partial_kernel(const T* __restrict__ X, int64_t ldx, int64_t nc,
+                                                          int64_t Tn, int L, double scale,
+                                                          const T* __restrict__ ring, T* __restrict__ P,
+                                                          const unsigned int* abort) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k = idx / nc, c = idx - k * nc;
+    if (k > L + 1 || aborted(abort)) return;
+    const T* __restrict__ xr = X + (size_t)c * ldx;
+    const T* __restrict__ rr = ring + (size_t)c * L;
+    T s = 0;
+    if (k == L + 1) {
+#pragma unroll 8
+        for (int64_t t = 0; t < Tn; ++t) s += lag_val(rr, xr, L, L + t, scale);
+    } else {
+#pragma unroll 8
+        for (int64_t t = 0; t < Tn; ++t) s += lag_val(rr, xr, L, L + t, scale) * lag_val(rr, xr, L, L + t - k, scale);
+    }
+    P[(size_t)k * nc + c] = s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void lag_finish_kernel(const T* __restrict__ X, int64_t ldx, int64_t nc,
+                                                         int64_t Tn, int L, double scale, T* __restrict__ ring,
+                                                         const T* __restrict__ P, T* __restrict__ sums,
+                                                         const unsigned int* abort) {
+    if (aborted(abort)) return;
+    if ((int)blockIdx.x >= L + 2) {  // ring update: ascending j reads index j + T > j, not yet written
+        const int64_t c = (int64_t)(blockIdx.x - (L + 2)) * blockDim.x + threadIdx.x;
+        if (c >= nc) return;
+        const T* __restrict__ xr = X + (size_t)c * ldx;
+        T* __restrict__ rr = ring + (size_t)c * L;
+        for (int j = 0; j < L; ++j) rr[j] = lag_val(rr, xr, L, j + Tn, scale);
+        return;
+    }
+    const int k = blockIdx.x;
+    T s = 0;
+    for (int64_t c = threadIdx.x; c < nc; c += 256) s += P[(size_t)k * nc + c];
+    __shared__ T red[256];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) sums[k] += red[0];
 }
 
 // ||v||^2 of rows (q / rb) * rstride + roff + q % rb of V (ld d), one wave per row,
@@ -2802,7 +2871,10 @@ hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt,
     znz = nullptr;
 #endif
     const int64_t chunk = 16384;  // multiple of 4
-    constexpr int RY = 4;  // rows per workgroup, vector path
+#ifndef LGS_MOM_RY
+#define LGS_MOM_RY 4
+#endif
+    constexpr int RY = LGS_MOM_RY;  // rows per workgroup, vector path
     const dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
     const dim3 gridv((unsigned)((n + chunk - 1) / chunk), (unsigned)((d + RY - 1) / RY));
     const int vw = zb == 2 ? 8 : 4;  // proposals per lane of the vector path
@@ -2831,6 +2903,24 @@ hipError_t gather_z(const void* Z, int zb, int64_t ldz, const int64_t* sel, int6
     if (nq <= 0) return hipSuccess;
     const dim3 grid((unsigned)((nq + 255) / 256), (unsigned)d);
     LGS_ZT(zb, ZT, LGS_ZT(ob, OT, hipLaunchKernelGGL((gather_z_kernel<ZT, OT>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, nq, q_per_chain, (const OT*)zs, zs_coord_major, nc, d, (OT*)out, out_coord_major, abort)));
+    return hipGetLastError();
+}
+
+hipError_t lag_update(const void* X, int is_f64, int64_t ldx, int64_t nc, int64_t Tn, int L, double scale,
+                      void* ring, void* sums, void* P, hipStream_t st, const unsigned int* abort) {
+    if (nc <= 0 || Tn <= 0 || L < 0) return hipSuccess;
+    const dim3 g1((unsigned)((nc * (L + 2) + 255) / 256)), g2((unsigned)(L + 2 + (nc + 255) / 256));
+    if (is_f64) {
+        hipLaunchKernelGGL(lag_partial_kernel<double>, g1, dim3(256), 0, st, (const double*)X, ldx, nc, Tn, L, scale,
+                           (const double*)ring, (double*)P, abort);
+        hipLaunchKernelGGL(lag_finish_kernel<double>, g2, dim3(256), 0, st, (const double*)X, ldx, nc, Tn, L, scale,
+                           (double*)ring, (const double*)P, (double*)sums, abort);
+    } else {
+        hipLaunchKernelGGL(lag_partial_kernel<int64_t>, g1, dim3(256), 0, st, (const int64_t*)X, ldx, nc, Tn, L,
+                           scale, (const int64_t*)ring, (int64_t*)P, abort);
+        hipLaunchKernelGGL(lag_finish_kernel<int64_t>, g2, dim3(256), 0, st, (const int64_t*)X, ldx, nc, Tn, L,
+                           scale, (int64_t*)ring, (const int64_t*)P, (int64_t*)sums, abort);
+    }
     return hipGetLastError();
 }
 
@@ -2947,8 +3037,9 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
                  hipStream_t st, const unsigned int* abort, const uint8_t* znz, const unsigned int* clive,
-                 int64_t clive_ld, double* VNP) {
+                 int64_t clive_ld, double* VNP, int64_t vn_n) {
     if (n <= 0) return hipSuccess;
+    if (vn_n <= 0) VNP = nullptr;
     if (d % 16 != 0 || LGS_BZ_TA != 1 || d > kOzMaxD) h16 = nullptr;  // history blocks must align with the chunks
 #ifdef LGS_BZ_NO_ZNZ
     znz = nullptr;
@@ -2958,10 +3049,16 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
 #ifdef LGS_BZ_NO_CLIVE
     clive = nullptr;
 #endif
+#ifdef LGS_DIAG_BZ_NO_VNP  // diagnostic builds only: epilogue cost of the ||v||^2 partial sums
+    VNP = nullptr;
+#endif
+#ifdef LGS_DIAG_BZ_NO_SEL  // diagnostic builds only (identity selections, e.g. acceptance 1): gather cost
+    sel = nullptr;
+#endif
     const int tx = ((d + 127) / 128 + LGS_BZ_TXPER - 1) / LGS_BZ_TXPER;  // coordinate-tile groups
     const int64_t ty = (n + 64 * LGS_BZ_TA - 1) / (64 * LGS_BZ_TA);
     const dim3 grid((unsigned)(tx * ((ty + 7) / 8) * 8));  // whole rounds of 8 XCDs (extra tiles exit)
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort, znz, clive, clive_ld, VNP));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort, znz, clive, clive_ld, VNP, vn_n));
     return hipGetLastError();
 }
 

@@ -56,7 +56,9 @@ class ImhkOutputs(ctypes.Structure):
     """struct lgs_imhk_outputs (include/lgs.h)."""
     _fields_ = [("logw_samples", ctypes.c_void_p), ("accepted", ctypes.c_void_p),
                 ("vnorm2_samples", ctypes.c_void_p), ("zk_samples", ctypes.c_void_p),
-                ("zk_index", ctypes.c_int64)]
+                ("zk_index", ctypes.c_int64), ("fn_chains", ctypes.c_int64),
+                ("lag_L", ctypes.c_int64), ("lag_z_ring", ctypes.c_void_p), ("lag_z_sums", ctypes.c_void_p),
+                ("lag_v_ring", ctypes.c_void_p), ("lag_v_sums", ctypes.c_void_p), ("lag_v_scale", ctypes.c_double)]
 
 
 class LgsError(RuntimeError):
@@ -258,12 +260,16 @@ class Context:
 
     def imhk(self, seed, first_chain, n_chains, first_step, n_steps, thin, z_state, logw_state,
              state_init, accepts, z_samples=None, v_samples=None, moments=None, flags=0,
-             logw_samples=None, accepted=None, vnorm2_samples=None, zk_samples=None, zk_index=0):
+             logw_samples=None, accepted=None, vnorm2_samples=None, zk_samples=None, zk_index=0,
+             fn_chains=0, lag=None):
         """lgs_imhk; with logw_samples (n_chains x n_steps/thin float64) or accepted
         (n_chains x n_steps uint8) lgs_imhk_trace, which also records each kept
         state's log weight and each step's accept decision; with vnorm2_samples /
         zk_samples (n_chains x n_steps/thin float64 / int64, device) lgs_imhk_ex, which
-        also gives ||v||^2 and coefficient zk_index of each kept state."""
+        also gives ||v||^2 and coefficient zk_index of each kept state (fn_chains > 0:
+        of the leading fn_chains chains only, arrays fn_chains x n_steps/thin); lag =
+        (L, z_ring, z_sums, v_ring, v_sums, v_scale): device buffers whose lag-0..L sums
+        of both series the call continues (include/lgs.h lgs_imhk_outputs.lag_L)."""
         zt = "int64" if flags & LGS_Z64 else "int32"
         _check_bufs(flags, self.device, ((z_state, zt, "z_state"), (logw_state, "float64", "logw_state"),
                                          (state_init, "int32", "state_init"), (accepts, "int64", "accepts"),
@@ -279,7 +285,12 @@ class Context:
             def v(a):
                 q = _ptr(a)
                 return None if q is None else q.value
-            out = ImhkOutputs(v(logw_samples), v(accepted), v(vnorm2_samples), v(zk_samples), int(zk_index))
+            lg = (0, None, None, None, None, 0.0) if lag is None else lag
+            if lag is not None:
+                _check_bufs(flags, self.device, ((lg[1], "int64", "lag z ring"), (lg[2], "int64", "lag z sums"),
+                                                 (lg[3], "float64", "lag v ring"), (lg[4], "float64", "lag v sums")))
+            out = ImhkOutputs(v(logw_samples), v(accepted), v(vnorm2_samples), v(zk_samples), int(zk_index),
+                              int(fn_chains), int(lg[0]), v(lg[1]), v(lg[2]), v(lg[3]), v(lg[4]), float(lg[5]))
             _check(_lib.lgs_imhk_ex(*args, ctypes.byref(out), int(flags)))
         elif logw_samples is None and accepted is None:
             _check(_lib.lgs_imhk(*args, int(flags)))

@@ -127,9 +127,11 @@ class LagSums:
         self.t, self.L = torch, L
         self.ring = torch.zeros((n_chains, L), dtype=dtype, device=device)
         self.have = 0
-        self.S = torch.zeros(L + 1, dtype=dtype, device=device)   # sum_t x_t x_{t-k}
+        # one buffer [S | S1] (the library's fused update adds to it in place)
+        self.sums = torch.zeros(L + 2, dtype=dtype, device=device)
+        self.S = self.sums[:L + 1]                                 # sum_t x_t x_{t-k}
         self.N = np.zeros(L + 1, dtype=np.int64)                  # pairs per lag
-        self.S1 = torch.zeros(1, dtype=dtype, device=device)
+        self.S1 = self.sums[L + 1:]
         self.n = 0
 
     def update(self, x):
@@ -191,7 +193,7 @@ class StreamingShard:
     single all-reduce (``covariance``)."""
 
     def __init__(self, advance: Callable, n_chains: int, d: int, *, binv_row, device, lag_chains: int = 1024,
-                 lags: int = 16, first_step: int = 1, gram_every: int = 0):
+                 lags: int = 16, first_step: int = 1, gram_every: int = 0, fused_lag: bool = True):
         import torch
         self.t = torch
         self.advance = advance
@@ -201,6 +203,7 @@ class StreamingShard:
         if gram_every and not hasattr(advance, "gram"):
             raise ValueError("gram_every needs an advance callable with a gram(G, S) method")
         self.gram_every = int(gram_every)
+        self.fused_lag = fused_lag
         self.binv = torch.as_tensor(np.asarray(binv_row, dtype=np.float64)).to(device)
         self.next_step = first_step
         # the per-block lag-sum update is ~20 small kernels; on a GPU it is replayed
@@ -218,6 +221,12 @@ class StreamingShard:
         self.mom = t.zeros(2 * self.d, dtype=t.int64, device=self.dev)
         self.lag_z = LagSums(t, self.lag_chains, self.lags, t.int64, self.dev)
         self.lag_v = LagSums(t, self.lag_chains, self.lags, t.float64, self.dev)
+        # an advance that continues the lag sums itself (gpu_advance: inside lgs_imhk_ex,
+        # before its final synchronisation) gets the sums' device buffers
+        self._fused_lag = False
+        if hasattr(self.advance, "bind_lag"):
+            self._fused_lag = self.advance.bind_lag(self.lag_z if self.fused_lag else None, self.lag_v,
+                                                    self.lag_chains, self.lags, 1e-6)
         self.steps_done = 0
         self.blocks = 0
         if self.gram_every:
@@ -232,7 +241,8 @@ class StreamingShard:
         self.steps_done += n_steps
         self.blocks += 1
         if v is not None:
-            self._lag_update(v)
+            if not (isinstance(v, dict) and v.get("lag_done")):
+                self._lag_update(v)
             self.lag_z.update_host(self.lag_chains, n_steps)
             self.lag_v.update_host(self.lag_chains, n_steps)
         if self.gram_every and self.blocks % self.gram_every == 0:
@@ -299,12 +309,14 @@ class StreamingShard:
 
 
 def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device, *, flags: int = 0,
-                block_steps: int = 0, want_v: bool = True):
+                block_steps: int = 0, want_v: bool = True, fn_chains: int = 0):
     """StreamingShard's advance over the HIP C-ABI: chain state resident on the
     device (coordinate-major z), one lgs_imhk call per block; v of every kept state
     into a preallocated (n_chains, block_steps, d) buffer.  The state tensors are
     exposed as ``advance.state``; ``advance.gram(G, S)`` adds sum z z^T / sum z of
-    the chains' current states (lgs_gram, exact int8-digit MFMA).
+    the chains' current states (lgs_gram, exact int8-digit MFMA).  The lag
+    functionals ("zk", "vn2") cover the leading ``fn_chains`` chains (0: all; a
+    StreamingShard reads its first ``lag_chains``).
 
     Streams: the library runs on a dedicated torch stream that waits (on the GPU,
     no host synchronisation) for everything the caller enqueued on its current
@@ -321,6 +333,7 @@ def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device,
           if want_v and block_steps else None,
           "zk": None, "vn2": None}
     fl = flags | _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR
+    nfn = n_chains if fn_chains <= 0 else min(int(fn_chains), n_chains)
     lib_stream = torch.cuda.Stream(device=device)
     ctx.set_stream(lib_stream.cuda_stream)
 
@@ -330,22 +343,35 @@ def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device,
     def _leave():
         torch.cuda.current_stream(device).wait_stream(lib_stream)
 
+    lag = {}
+
+    def bind_lag(lag_z, lag_v, lag_chains, L, v_scale):
+        """StreamingShard hands over its LagSums: lgs_imhk_ex continues them (fused);
+        lag_z None: unbind (the shard updates its sums from the returned series)."""
+        lag.clear()
+        if lag_z is None or not want_v or lag_chains != nfn:  # (the library's series: exactly nfn chains)
+            return False
+        lag.update(z=lag_z, v=lag_v, L=int(L), scale=float(v_scale))
+        return True
+
     def advance(first_step, n_steps, acc, mom):
         v = st["v"]
         if want_v and (v is None or v.shape[1] != n_steps):
             v = st["v"] = torch.empty((n_chains, n_steps, d), dtype=torch.float64, device=device)
         if want_v and (st["zk"] is None or st["zk"].shape[1] != n_steps):
-            st["zk"] = torch.empty((n_chains, n_steps), dtype=torch.int64, device=device)
-            st["vn2"] = torch.empty((n_chains, n_steps), dtype=torch.float64, device=device)
+            st["zk"] = torch.empty((nfn, n_steps), dtype=torch.int64, device=device)
+            st["vn2"] = torch.empty((nfn, n_steps), dtype=torch.float64, device=device)
         _enter()
         # the lag functionals z_{d-1} and ||v||^2 of every kept state come from the
         # library (coefficient store / B z epilogue), not from re-reading v
         ctx.imhk(seed, first_chain, n_chains, first_step, n_steps, 1, st["z"], st["lw"], st["init"], acc,
                  v_samples=v if want_v else None, moments=mom, flags=fl,
                  vnorm2_samples=st["vn2"] if want_v else None, zk_samples=st["zk"] if want_v else None,
-                 zk_index=d - 1)
+                 zk_index=d - 1, fn_chains=nfn,
+                 lag=(lag["L"], lag["z"].ring, lag["z"].sums, lag["v"].ring, lag["v"].sums, lag["scale"])
+                 if lag else None)
         _leave()
-        return {"v": v, "zk": st["zk"], "vn2": st["vn2"]} if want_v else None
+        return {"v": v, "zk": st["zk"], "vn2": st["vn2"], "lag_done": bool(lag)} if want_v else None
 
     def gram(G, S):
         _enter()
@@ -354,6 +380,7 @@ def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device,
 
     advance.state = st
     advance.gram = gram
+    advance.bind_lag = bind_lag
     advance.stream = lib_stream
     return advance
 

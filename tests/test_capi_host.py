@@ -156,3 +156,15 @@ def test_buffer_checks_reject_mismatched_dtype_and_memory():
         _capi._check_bufs(_capi.LGS_DEVICE_PTRS, 0, ((torch.zeros(3, dtype=torch.float64), "float64", "v"),))
     with pytest.raises(ValueError, match="contiguous"):
         _capi._ptr(torch.zeros((4, 4))[:, 1])
+
+
+def test_imhk_outputs_struct_matches_header():
+    """ctypes mirror of struct lgs_imhk_outputs: same field names, order and size."""
+    import ctypes
+    import re
+    from lgs_amd import _capi
+    hdr = open(os.path.join(REPO, "include", "lgs.h")).read()
+    body = re.search(r"typedef struct lgs_imhk_outputs \{(.*?)\} lgs_imhk_outputs;", hdr, re.S).group(1)
+    names = re.findall(r"\*?(\w+);", body)
+    assert names == [f[0] for f in _capi.ImhkOutputs._fields_]
+    assert ctypes.sizeof(_capi.ImhkOutputs) == 8 * len(names)

@@ -127,3 +127,79 @@ def test_imhk_ex_functionals_equal_recomputation(cfg):
         assert torch.equal(vn2, (vs * vs).sum(-1))
         assert torch.equal(zk, zs[:, :, d - 1].long())
         assert torch.equal(vs, zs.double() @ torch.as_tensor(B, device=dev).T)
+
+
+@pytest.mark.parametrize("fn", [1, 100, 511])
+def test_imhk_ex_functionals_of_leading_chains(fn):
+    """fn_chains: the functionals of the leading fn chains only (fn x n_keep arrays),
+    equal to the all-chains run's first rows; nothing written past them."""
+    import torch
+    from lgs_amd import _capi
+    from lgs_amd.lattices import build_config
+    import lgs_oracle
+    lat, sigma = build_config("C3_ntru512")
+    B = lat.basis
+    R, cp = lgs_oracle.qr_prepare(B)
+    d = B.shape[0]
+    ctx = _capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    nc, T = 512, 8
+    dev = "cuda:0"
+    res = []
+    for f in (0, fn):
+        z = torch.zeros((nc, d), dtype=torch.int32, device=dev)
+        lw = torch.zeros(nc, dtype=torch.float64, device=dev)
+        init = torch.zeros(nc, dtype=torch.int32, device=dev)
+        acc = torch.zeros(nc, dtype=torch.int64, device=dev)
+        rows = nc if f == 0 else f + 1  # (one guard row)
+        vs = torch.empty((nc, T, d), dtype=torch.float64, device=dev)
+        vn2 = torch.full((rows, T), -1.0, dtype=torch.float64, device=dev)
+        zk = torch.full((rows, T), -7, dtype=torch.int64, device=dev)
+        ctx.imhk(9, 0, nc, 1, T, 1, z, lw, init, acc, v_samples=vs, flags=_capi.LGS_DEVICE_PTRS,
+                 vnorm2_samples=vn2, zk_samples=zk, zk_index=d - 1, fn_chains=f)
+        torch.cuda.synchronize()
+        res.append((vs, vn2, zk))
+    (va, na, ka), (vb, nb, kb) = res
+    assert torch.equal(va, vb)
+    assert torch.equal(nb[:fn], na[:fn]) and torch.equal(kb[:fn], ka[:fn])
+    assert torch.equal(na, (va * va).sum(-1))
+    assert bool((nb[fn] == -1.0).all()) and bool((kb[fn] == -7).all())
+
+
+def _lag_shard(fused: bool):
+    import torch
+    from lgs_amd import _capi
+    from lgs_amd import distributed as D
+    from lgs_amd.lattices import build_config
+    import lgs_oracle
+    lat, sigma = build_config("C3_ntru512")
+    B = lat.basis
+    R, cp = lgs_oracle.qr_prepare(B)
+    d = B.shape[0]
+    ctx = _capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    dev = torch.device("cuda", 0)
+    nc, T = 1024, 8
+    adv = D.gpu_advance(ctx, 12, 0, nc, d, dev, block_steps=T, fn_chains=300)
+    sh = D.StreamingShard(adv, nc, d, binv_row=np.linalg.inv(B)[d - 1], device=dev, lag_chains=300, lags=11,
+                          fused_lag=fused)
+    assert sh._fused_lag == fused
+    for _ in range(3):  # T = 8 < L = 11: the ring carries values across blocks
+        sh.step(T)
+    st = sh.reduce()
+    torch.cuda.synchronize()
+    return {k: ([x.cpu().numpy().copy() for x in v] if isinstance(v, list) else v.cpu().numpy().copy())
+            for k, v in st.items()}
+
+
+def test_fused_lag_sums_equal_torch_update():
+    """lgs_imhk_ex's lag sums (lag_L, inside the call) equal LagSums' torch update on
+    the returned series: int64 z series exactly, the fp64 ||v||^2 series to 1e-12."""
+    a, b = _lag_shard(True), _lag_shard(False)
+    for k in ("accepts", "moments"):
+        assert np.array_equal(a[k], b[k])
+    for x, y in zip(a["lag_z"], b["lag_z"]):
+        assert np.array_equal(x, y)
+    for x, y in zip(a["lag_v"], b["lag_v"]):
+        np.testing.assert_allclose(x, y, rtol=1e-12, atol=0)
+    assert a["lag_z"][0][0] > 0

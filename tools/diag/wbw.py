@@ -3,9 +3,11 @@ judging the bz_i8 epilogue."""
 import torch
 n = 1 << 28  # 2 GiB of fp64
 x = torch.empty(n, dtype=torch.float64, device="cuda")
+xl = torch.empty(n * 4, dtype=torch.float64, device="cuda")  # 8 GiB: the bench's B z output per step
 y = torch.empty(n // 2, dtype=torch.float64, device="cuda")
 z = torch.empty(n // 2, dtype=torch.float64, device="cuda")
 for name, fn, nbytes in [("fill_2GiB", lambda: x.fill_(1.0), 8 * n),
+                         ("fill_8GiB", lambda: xl.fill_(1.0), 32 * n),
                          ("copy_1GiB", lambda: y.copy_(z), 8 * n)]:
     for _ in range(3):
         fn()
