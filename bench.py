@@ -7,10 +7,11 @@ sigma = 165.7, IMHK with 2^14 chains per GPU.  One bench step = one
 2^20 Klein proposals (back-substitution + SampleZ + importance weight), the
 Metropolis scan, exact integer moments, and the lattice points v = B z of every
 kept state (thin = 1), all resident in HBM; then the lag-L autocovariance sums
-of two scalar functionals of the kept states (a coefficient and ||v||^2, SURVEY
-§8e) are accumulated on the device, both produced by the library itself
-(lgs_imhk_ex: ||v||^2 in the B z epilogue, the coefficient from the proposal
-store), and the exact sum z z^T of the chains' states after the step (lgs_gram;
+of two scalar functionals of the first 1024 chains' kept states (a coefficient and
+||v||^2) are continued on the device inside the same library call
+(lgs_imhk_ex: ||v||^2 in the B z epilogue for those chains, the coefficient from
+the proposal store, the lag sums before the call's synchronisation), and the
+exact sum z z^T of the chains' states after the step (lgs_gram;
 the job's empirical covariance, base.py:154-160, comes back from the same single
 all-reduce).  The coefficient is z_{d-1}, the first one Klein decides (for the
 NTRU / q-ary bases z_0 is a q-coordinate with sigma_0 ~ 0.01, identically 0).
@@ -26,10 +27,11 @@ every accumulator (acceptance, exact moments, the lag sums), inside the timed
 region.  The 8-GPU workload of BASELINE configs[3] is
 ``--gpus 8 --config C4_qary1024`` (2^15 chains per GPU, 2^18 in all).
 
-Also reported: the dominant kernel's roofline (the Klein sampler, HIP-event
-timed on its launch stream; executed-work and HBM counters from the committed
-rocprofv3 profile of this command, profiles/r0*_klein_counters.json, used only
-when its build_id is the loaded library's), the
+Also reported: the dominant kernel's roofline (the Klein sampler: executed-work
+and HBM counters and the launch's rocprof duration from the committed rocprofv3
+profile of this command, profiles/r0*_klein_counters.json, used only when its
+build_id is the loaded library's; the HIP-event time of the same kernel in this
+run beside it), the
 certificate's redo count, a parity check of the timed run's final chain states
 against the oracle, and the CPU baselines (the C oracle over the host cores and
 the NumPy restatement of the reference's loop, one process per core).

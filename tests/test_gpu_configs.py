@@ -88,7 +88,10 @@ def test_imhk_acceptance_vs_cpu(oracle, cfg, nc, m):
     """IMHK acceptance against the CPU reference (imhk.py:141-177), north_star
     'acceptance within +-1 % of CPU reference', at C3, C4 and C5:
     * reference-mode weights: every proposal accepted on the GPU (1.0 exactly),
-      as in the reference (its weight is a constant up to rounding);
+      as in the reference (its weight is a constant up to rounding), and the first m
+      chains' accept counts, final states and log weights equal to the oracle's in
+      reference mode -- the coarse q-panel far field and the q-panel skip move the
+      weights' rounding only (ADVICE round 3);
     * Wang-Ling weights: the oracle runs the first m chains x 4 steps on the same
       counters -- every accept decision and final state is bit-equal -- and the
       GPU's acceptance over all nc chains is within 1 % (absolute) of the oracle's
@@ -108,9 +111,14 @@ def test_imhk_acceptance_vs_cpu(oracle, cfg, nc, m):
         acc = torch.zeros(nc, dtype=torch.int64, device="cuda")
         f = _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR | (_capi.LGS_WANG_LING if wl else 0)
         ctx.imhk(seed, 0, nc, 1, T, 1, z, lw, init, acc, flags=f)
-        res[wl] = (acc.cpu().numpy(), z[:, :m].cpu().numpy().T)
+        res[wl] = (acc.cpu().numpy(), z[:, :m].cpu().numpy().T, lw[:m].cpu().numpy())
     assert res[False][0].sum() == nc * T  # reference mode: acceptance 1.0
-    acc_wl, z_wl = res[True]
+    zr, lwr, accr = oracle.imhk_parallel(R, cp, B, sigma, m, T, seed=seed, first_step=1,
+                                         mode=oracle.IMHK_REFERENCE, threads=16)
+    assert np.array_equal(res[False][0][:m], accr)
+    assert np.array_equal(res[False][1], zr)
+    np.testing.assert_allclose(res[False][2], lwr, rtol=1e-12, atol=1e-9)
+    acc_wl, z_wl, _ = res[True]
     zo, _, acco = oracle.imhk_parallel(R, cp, B, sigma, m, T, seed=seed, first_step=1,
                                        mode=oracle.IMHK_WANG_LING, threads=16)
     assert np.array_equal(acc_wl[:m], acco)  # bit-equal decisions on the CPU subset
