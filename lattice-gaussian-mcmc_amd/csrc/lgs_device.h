@@ -54,8 +54,10 @@ __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
         }
-#ifndef LGS_PHILOX_MULHI
+#ifdef LGS_PHILOX_MAD64
         // one 32x32->64 multiply (v_mad_u64_u32) per product instead of mul_lo + mul_hi
+        // (round 4: the mul_lo / mul_hi pair below takes 13 fewer spilled VGPRs in the
+        // Klein kernel and runs it 2-4 % faster, profiles/r04ab_*, r04ac_*)
         const uint64_t m0 = (uint64_t)0xD2511F53u * c0;
         const uint64_t m1 = (uint64_t)0xCD9E8D57u * c2;
         const uint32_t lo0 = (uint32_t)m0, hi0 = (uint32_t)(m0 >> 32);

@@ -154,10 +154,10 @@ __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double
 // coordinate's step, before anything branches on it: one LDS round trip per
 // coordinate instead of one per use site (mean, kind, window, polynomials,
 // weight terms, near-field coefficients), each behind the previous branch.
-// The capped kind's erfinv coefficients come along as scalar loads (LGS_CAP_RI_PRE).
-#ifndef LGS_CAP_NO_RI_PRE
-#define LGS_CAP_RI_PRE 1
-#endif
+// (LGS_CAP_RI_PRE: the capped kind's erfinv coefficients come along as scalar loads;
+// round 4: off by default -- without it, and with the Philox products as mul_lo /
+// mul_hi pairs, the kernel spills 49 instead of 63 VGPRs and runs C2 / C3 / C4 / C5
+// 4 / 2 / 3 / 3 % faster, outputs identical, profiles/r04ac_kbench_mulhi_noripre.log)
 constexpr int kRecHot = kRecRs + 16;  // through the 15 near-field coefficients (44 doubles)
 struct RecRegs {
     double v[kRecHot];
