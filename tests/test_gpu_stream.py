@@ -203,3 +203,53 @@ def test_fused_lag_sums_equal_torch_update():
     for x, y in zip(a["lag_v"], b["lag_v"]):
         np.testing.assert_allclose(x, y, rtol=1e-12, atol=0)
     assert a["lag_z"][0][0] > 0
+
+
+def test_imhk_ex_lag_sums_with_thinning_across_calls():
+    """lgs_imhk_ex lag_L on its own (no StreamingShard): thin = 2, two calls whose
+    series continue through the caller's ring; the sums equal numpy's over the
+    concatenated kept-state series (int64 exactly, the scaled ||v||^2 to 1e-12)."""
+    import torch
+    from lgs_amd import _capi
+    from lgs_amd.lattices import build_config
+    import lgs_oracle
+    lat, sigma = build_config("C2_qary128")
+    B = lat.basis
+    R, cp = lgs_oracle.qr_prepare(B)
+    d = B.shape[0]
+    ctx = _capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    nc, steps, thin, L, fn = 300, 12, 2, 5, 200
+    dev = "cuda:0"
+    z = torch.zeros((d, nc), dtype=torch.int32, device=dev)
+    lw = torch.zeros(nc, dtype=torch.float64, device=dev)
+    init = torch.zeros(nc, dtype=torch.int32, device=dev)
+    acc = torch.zeros(nc, dtype=torch.int64, device=dev)
+    zr = torch.zeros((fn, L), dtype=torch.int64, device=dev)
+    zsum = torch.zeros(L + 2, dtype=torch.int64, device=dev)
+    vr = torch.zeros((fn, L), dtype=torch.float64, device=dev)
+    vsum = torch.zeros(L + 2, dtype=torch.float64, device=dev)
+    xs_z, xs_v = [], []
+    for call in range(2):
+        nk = steps // thin
+        vs = torch.empty((nc, nk, d), dtype=torch.float64, device=dev)
+        vn2 = torch.empty((fn, nk), dtype=torch.float64, device=dev)
+        zk = torch.empty((fn, nk), dtype=torch.int64, device=dev)
+        ctx.imhk(5, 0, nc, 1 + call * steps, steps, thin, z, lw, init, acc, v_samples=vs,
+                 flags=_capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR | _capi.LGS_WANG_LING,
+                 vnorm2_samples=vn2, zk_samples=zk, zk_index=d - 1, fn_chains=fn,
+                 lag=(L, zr, zsum, vr, vsum, 1e-6))
+        torch.cuda.synchronize()
+        xs_z.append(zk.cpu().numpy())
+        xs_v.append(vn2.cpu().numpy() * 1e-6)
+    for xs, got, exact in ((np.concatenate(xs_z, 1), zsum.cpu().numpy(), True),
+                           (np.concatenate(xs_v, 1), vsum.cpu().numpy(), False)):
+        n = xs.shape[1]
+        want = [sum((xs[:, t] * xs[:, t - k]).sum() for t in range(k, n)) for k in range(L + 1)]
+        want.append(xs.sum())
+        want = np.array(want, dtype=xs.dtype)
+        if exact:
+            assert np.array_equal(got, want)
+        else:
+            np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)
+    assert np.array_equal(zr.cpu().numpy(), np.concatenate(xs_z, 1)[:, -L:])
