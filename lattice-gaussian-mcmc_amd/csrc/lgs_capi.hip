@@ -155,6 +155,10 @@ struct lgs_ctx {
     bool has_q = false, has_binv = false;
     std::vector<Timer> pending;
     std::vector<hipEvent_t> pool;
+    // lgs_imhk on a caller's stream (early check): the flag words as of a block's
+    // abort producers, copied into pinned host memory, and the event after that copy
+    unsigned int* fw_host = nullptr;
+    hipEvent_t fw_ev = nullptr;
 };
 
 namespace {
@@ -250,12 +254,16 @@ void fold_counters(lgs_ctx* c, const unsigned int* fw) {
     }
 }
 
-// fw_known: the caller has synchronised and read the flag words (one device-to-host
-// copy per call instead of one per check: each is a round trip the GPU idles through).
-int finish(lgs_ctx* c, const unsigned int* fw_known = nullptr) {  // sync, fold timers, report kernel flags
-    int rc0 = settle_bz(c, fw_known);
-    if (rc0) return rc0;
+// Folds the finished launch timers into the context's totals; a timer whose end
+// event is still pending (the early check leaves a block's later launches running)
+// stays for a later call or lgs_timing_get.
+void fold_timers(lgs_ctx* c) {
+    size_t keep = 0;
     for (auto& t : c->pending) {
+        if (hipEventQuery(t.b) != hipSuccess) {
+            c->pending[keep++] = t;
+            continue;
+        }
         float ms = 0;
         if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
             c->t_ms[t.kernel] += ms;
@@ -264,7 +272,18 @@ int finish(lgs_ctx* c, const unsigned int* fw_known = nullptr) {  // sync, fold 
         c->pool.push_back(t.a);
         c->pool.push_back(t.b);
     }
-    c->pending.clear();
+    c->pending.resize(keep);
+}
+
+// fw_known: the caller has synchronised and read the flag words (one device-to-host
+// copy per call instead of one per check: each is a round trip the GPU idles through).
+// clear_all: reset every flag word, word 0 included, behind the work already enqueued
+// (the early check: word 0 may still receive the digit-range bit of a B z whose
+// device-gated replay follows it).
+int finish(lgs_ctx* c, const unsigned int* fw_known = nullptr, bool clear_all = false) {  // sync, fold timers, report kernel flags
+    int rc0 = settle_bz(c, fw_known);
+    if (rc0) return rc0;
+    fold_timers(c);
     unsigned int fw[lgs::kFlagWords] = {};
     if (fw_known)
         memcpy(fw, fw_known, sizeof(fw));
@@ -279,7 +298,9 @@ int finish(lgs_ctx* c, const unsigned int* fw_known = nullptr) {  // sync, fold 
     c->n_qskip += fw[lgs::kFlagWordQSkip];
     bool any = false;
     for (int k = 1; k < lgs::kFlagWords; ++k) any |= fw[k] != 0;
-    if (any)  // ordered before the next launches
+    if (clear_all)
+        HIP_TRY(hipMemsetAsync(c->flags.p, 0, lgs::kFlagWords * sizeof(unsigned int), c->stream));
+    else if (any)  // ordered before the next launches
         HIP_TRY(hipMemsetAsync((unsigned int*)c->flags.p + 1, 0, (lgs::kFlagWords - 1) * sizeof(unsigned int),
                                c->stream));
     if (f & lgs::kFlagNonFinite)
@@ -296,12 +317,24 @@ int finish(lgs_ctx* c, const unsigned int* fw_known = nullptr) {  // sync, fold 
 // attempt is discarded (its B z launches, its verification count beyond the
 // checkpoint, its |z| maximum), the context switches to the wider store / the fp64
 // far field, and redo is set.  Otherwise the usual finish().
-int finish_or_redo(lgs_ctx* c, bool oz_used, int& zb, bool& redo) {
+//
+// early (lgs_imhk on a caller's stream): the flag words were copied into fw_host
+// right after the block's abort producers (its Klein launches, the carried-in
+// states) and the block's later launches are already enqueued; wait for that copy
+// only, so the caller's next work is enqueued while they run.  Those later launches
+// write no flag the host reads (reference weights: no accept counters; B z's digit
+// range is replayed on the device), and every flag word is reset behind them.
+int finish_or_redo(lgs_ctx* c, bool oz_used, int& zb, bool& redo, bool early = false) {
     redo = false;
-    HIP_TRY(hipStreamSynchronize(c->stream));
     unsigned int fw[lgs::kFlagWords];
-    HIP_TRY(hipMemcpy(fw, c->flags.p, sizeof(fw), hipMemcpyDeviceToHost));
-    if (!(fw[0] & lgs::kAbortMask)) return finish(c, fw);
+    if (early) {
+        HIP_TRY(hipEventSynchronize(c->fw_ev));
+        memcpy(fw, c->fw_host, sizeof(fw));
+    } else {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpy(fw, c->flags.p, sizeof(fw), hipMemcpyDeviceToHost));
+    }
+    if (!(fw[0] & lgs::kAbortMask)) return finish(c, fw, early);
     c->pending_i8.clear();
     for (auto& t : c->pending) {  // the aborted attempt's timers are not kept
         c->pool.push_back(t.a);
@@ -471,7 +504,7 @@ int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
 int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
            int64_t rb = 0, int64_t rstride = 0, int64_t roff = 0, const int64_t* sel = nullptr,
            bool after_klein = false, const unsigned int* abort = nullptr, double* VN = nullptr,
-           int64_t vn_n = -1) {
+           int64_t vn_n = -1, bool device_replay = false) {
     if (!c->has_B) return fail(LGS_ERR_STATE, "lattice points need B (lgs_set_basis B != NULL)");
     if (vn_n < 0 || vn_n > n) vn_n = n;  // ||v||^2 of the leading vn_n rows only
     if (vn_n == 0) VN = nullptr;
@@ -501,6 +534,15 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
                                after_klein && c->hist.Z == Z && Z ? c->hist.clive : nullptr, c->hist.clive_ld,
                                VNP, vn_n));
     if (VN) HIP_TRY(lgs::launch::vnorm2_reduce(VNP, (int)c->d, vn_n, b.rb, b.rstride, b.roff, VN, c->stream, abort));
+    if (device_replay) {  // the fp64 replay enqueued now, run only if the digit-range flag is set
+        const unsigned int* need = c->flags.as<unsigned int>();
+        HIP_TRY(lgs::launch::bz(b.Z, b.zb, b.ldz, b.sel, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
+                                b.rstride, b.roff, c->stream, abort, need));
+        if (VN)
+            HIP_TRY(lgs::launch::vnorm2_rows(b.V, (int)c->d, vn_n, b.rb, b.rstride, b.roff, VN, c->stream, abort,
+                                             need));
+        return LGS_OK;
+    }
     c->pending_i8.push_back(b);
     return LGS_OK;
 }
@@ -609,6 +651,8 @@ int lgs_destroy(lgs_ctx* c) {
         (void)hipEventDestroy(t.b);
     }
     for (auto e : c->pool) (void)hipEventDestroy(e);
+    if (c->fw_ev) (void)hipEventDestroy(c->fw_ev);
+    if (c->fw_host) (void)hipHostFree(c->fw_host);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
     return LGS_OK;
@@ -1177,6 +1221,18 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
     // Wang-Ling weights of the blocked kernels carry a bounded error: certify each
     // accept decision against it (LGS_EXACT_ORDER weights are the reference's)
     const bool certw = wl && !exact;
+    // Early check (device pointers on a caller's stream -- lgs_set_stream orders the
+    // caller's work after ours): each block waits only for its abort producers' flag
+    // words, not for its accept / moments / B z / gathers, so the caller's next work
+    // is enqueued while those run.  Not with the certified Wang-Ling accept (its
+    // counters come from the accept kernel).  Timers of the later launches are folded
+    // once they finish (fold_timers).  LGS_NO_EARLY_CHECK=1: A/B.
+    static const bool no_early = getenv("LGS_NO_EARLY_CHECK") && atoi(getenv("LGS_NO_EARLY_CHECK")) == 1;
+    const bool early = dev && c->stream != c->own && !certw && !no_early;
+    if (early && !c->fw_host) {
+        HIP_TRY(hipHostMalloc((void**)&c->fw_host, 4 * lgs::kFlagWords, hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&c->fw_ev, hipEventDisableTiming));
+    }
 
     // ---- block of T steps (a multiple of thin) per Klein launch
     int64_t T = std::max<int64_t>(1, c->max_props / nc);
@@ -1290,6 +1346,10 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
         // chain states carried into the block's store (a state beyond 16 bits flags kFlagCarry16)
         if (carry && kb > 0)
             HIP_TRY(lgs::launch::carry_cols(zs, ob, cm, nc, (int)d, c->Z.p, zb, ldzb, npb, c->stream, fl));
+        if (early) {  // every abort producer of the block is enqueued: its flag words for the host
+            HIP_TRY(hipMemcpyAsync(c->fw_host, fl, 4 * lgs::kFlagWords, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipEventRecord(c->fw_ev, c->stream));
+        }
         if (moments) HIP_TRY(hipMemsetAsync(c->cnt.p, 0, (size_t)npb * 4, c->stream));
         lgs::AcceptArgs aa{};
         aa.nc = nc;
@@ -1356,7 +1416,7 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             if (v_samples) {  // rows (chain, first_keep + k) of the n_chains x n_keep x d output,
                               // read straight from the proposal store through the selections
                 if ((rc = run_bz(c, c->Z.p, zb, ldzb, nq, v_samples, kb, n_keep, first_keep,
-                                 c->sel.as<int64_t>(), true, fl, vnorm2_samples, fn_chains * kb)))
+                                 c->sel.as<int64_t>(), true, fl, vnorm2_samples, fn_chains * kb, early)))
                     return rc;
             }
             if (zk_samples)  // (the leading fn_chains chains' kept states: q < fn_chains * kb)
@@ -1391,7 +1451,7 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, ldzb, c->fsel.as<int64_t>(), nc, 1, zs, ob, cm, nc,
                                           (int)d, zs, cm, c->stream, fl));
         bool redo = false;
-        if ((rc = finish_or_redo(c, oz_used, zb, redo))) return rc;
+        if ((rc = finish_or_redo(c, oz_used, zb, redo, early))) return rc;
         if (redo) continue;  // same block again (block 0: its initial draws too)
         t0 += T;
     }
@@ -1448,6 +1508,10 @@ int lgs_sample_z(lgs_ctx* c, int64_t n, const double* mu, const double* sigma, c
 int lgs_timing_enable(lgs_ctx* c, int enable) {
     int rc = check_ctx(c, false);
     if (rc) return rc;
+    if (!c->pending.empty()) {  // timers still running belong to the old totals
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        fold_timers(c);
+    }
     c->timing = enable != 0;
     for (int k = 0; k < 7; ++k) {
         c->t_ms[k] = 0;
@@ -1459,6 +1523,12 @@ int lgs_timing_enable(lgs_ctx* c, int enable) {
 int lgs_timing_get(lgs_ctx* c, int kernel, double* ms, int64_t* n) {
     if (!c) return fail(LGS_ERR_INVALID, "null context");
     if (kernel < 0 || kernel > 6) return fail(LGS_ERR_INVALID, "kernel id 0..6");
+    if (!c->pending.empty()) {  // launches of an early-checked call may still be running
+        int rc = check_ctx(c, false);
+        if (rc) return rc;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        fold_timers(c);
+    }
     if (ms) *ms = c->t_ms[kernel];
     if (n) *n = c->t_n[kernel];
     return LGS_OK;

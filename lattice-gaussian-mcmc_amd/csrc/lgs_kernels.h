@@ -284,7 +284,7 @@ hipError_t to_coord_major(const void* in, int ib, int64_t n, int d, void* Z, int
 // V row of sample s: (s / rb) * rstride + roff + s % rb (rb = n, rstride = roff = 0: row s)
 hipError_t bz(const void* Z, int zb, int64_t ldz, const int64_t* sel, const double* BT, int d,
               int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
-              hipStream_t st, const unsigned int* abort = nullptr);
+              hipStream_t st, const unsigned int* abort = nullptr, const unsigned int* need = nullptr);
 hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const int* kchunk,
                  const int* koff, const int8_t* Bd1, const int8_t* Bd0, int dc, int d, int64_t n,
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
@@ -307,7 +307,7 @@ hipError_t coord_gather(const void* Z, int zb, int64_t ldz, const int64_t* sel, 
                         const void* zs, int ob, int zs_coord_major, int64_t nc, int d, int k, int64_t* out,
                         int64_t rb, int64_t rstride, int64_t roff, hipStream_t st, const unsigned int* abort);
 hipError_t vnorm2_rows(const double* V, int d, int64_t n, int64_t rb, int64_t rstride, int64_t roff, double* VN,
-                       hipStream_t st);
+                       hipStream_t st, const unsigned int* abort = nullptr, const unsigned int* need = nullptr);
 // ---- decoding
 // V (row-major n x d) = rows s: sum_c MT[c][r] X[c][s], X coordinate-major fp64 (fp64 MFMA)
 hipError_t gemm_f64(const double* X, int64_t ldx, const double* MT, int d, int64_t n, double* V,

@@ -1727,6 +1727,11 @@ __global__ __launch_bounds__(256) void samplez_probe_kernel(const double* __rest
 __device__ __forceinline__ bool aborted(const unsigned int* abort) {
     return abort && (*(const volatile unsigned int*)abort & kAbortMask) != 0u;
 }
+// need: a device-gated replay (lgs_imhk without a host wait on B z) runs only when
+// the int8-digit B z before it flagged a coefficient beyond its digits
+__device__ __forceinline__ bool not_needed(const unsigned int* need) {
+    return need && (*(const volatile unsigned int*)need & kFlagI8Range) == 0u;
+}
 
 __global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2287,16 +2292,19 @@ __global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, 
                                                       const double* __restrict__ BT, int d,
                                                       int64_t n, double* __restrict__ V,
                                                       int64_t ldv, int64_t rb, int64_t rstride,
-                                                      int64_t roff, const unsigned int* abort) {
-    if (aborted(abort)) return;  // (whole grid) the selections were not written
+                                                      int64_t roff, const unsigned int* abort,
+                                                      const unsigned int* need) {
+    if (aborted(abort) || not_needed(need)) return;  // (whole grid) the selections were not written
     constexpr int BM = 64, BN = 64, KC = 16, LDP = 80;  // LDP: padded row (doubles)
     __shared__ double As[KC][LDP];
     __shared__ double Bs[KC][LDP];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
-    const int64_t s0 = (int64_t)blockIdx.x * BM;
     const int r0 = blockIdx.y * BN;
+    // sample tiles strided over the grid (one per workgroup except in the gated
+    // replay's small grid, which must not cost a full-size dispatch when not needed)
+    for (int64_t s0 = (int64_t)blockIdx.x * BM; s0 < n; s0 += (int64_t)gridDim.x * BM) {
     d4_t acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -2344,6 +2352,7 @@ __global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, 
                     V[(size_t)row * ldv + r] = acc[a][b][reg];
                 }
             }
+    }
 }
 
 // ------------------------------------------------------------ B z, exact int8 MFMA
@@ -2754,17 +2763,20 @@ __global__ __launch_bounds__(256) void lag_finish_kernel(const T* __restrict__ X
 // sums them in its epilogue).  Integral v: exact in any order.
 __global__ __launch_bounds__(256) void vnorm2_rows_kernel(const double* __restrict__ V, int d, int64_t n,
                                                           int64_t rb, int64_t rstride, int64_t roff,
-                                                          double* __restrict__ VN) {
-    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                          double* __restrict__ VN, const unsigned int* abort,
+                                                          const unsigned int* need) {
     const int lane = threadIdx.x & 63;
-    if (q >= n) return;
-    const int64_t row = (q / rb) * rstride + roff + q % rb;
-    const double* __restrict__ vr = V + (size_t)row * d;
-    double acc = 0.0;
-    for (int j = lane; j < d; j += 64) acc = fma(vr[j], vr[j], acc);
+    if (aborted(abort) || not_needed(need)) return;
+    // rows strided over the grid (the gated replay launches a small one)
+    for (int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); q < n; q += (int64_t)gridDim.x * 4) {
+        const int64_t row = (q / rb) * rstride + roff + q % rb;
+        const double* __restrict__ vr = V + (size_t)row * d;
+        double acc = 0.0;
+        for (int j = lane; j < d; j += 64) acc = fma(vr[j], vr[j], acc);
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-    if (lane == 0) VN[row] = acc;
+        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+        if (lane == 0) VN[row] = acc;
+    }
 }
 
 // ============================================================ launchers
@@ -2942,9 +2954,11 @@ hipError_t vnorm2_reduce(const double* VNP, int d, int64_t n, int64_t rb, int64_
 }
 
 hipError_t vnorm2_rows(const double* V, int d, int64_t n, int64_t rb, int64_t rstride, int64_t roff, double* VN,
-                       hipStream_t st) {
+                       hipStream_t st, const unsigned int* abort, const unsigned int* need) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(vnorm2_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, V, d, n, rb, rstride, roff, VN);
+    const int64_t nb = (n + 3) / 4;
+    hipLaunchKernelGGL(vnorm2_rows_kernel, dim3((unsigned)(need ? std::min<int64_t>(nb, 1024) : nb)), dim3(256), 0, st,
+                       V, d, n, rb, rstride, roff, VN, abort, need);
     return hipGetLastError();
 }
 
@@ -2996,10 +3010,11 @@ hipError_t to_coord_major(const void* in, int ib, int64_t n, int d, void* Z, int
 
 hipError_t bz(const void* Z, int zb, int64_t ldz, const int64_t* sel, const double* BT, int d,
               int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
-              hipStream_t st, const unsigned int* abort) {
+              hipStream_t st, const unsigned int* abort, const unsigned int* need) {
     if (n <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_gemm_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, BT, d, n, V, ldv, rb, rstride, roff, abort));
+    const int64_t nbx = (n + 63) / 64;  // (gated replay: 128 x-tiles, each workgroup loops)
+    const dim3 grid((unsigned)(need ? std::min<int64_t>(nbx, 128) : nbx), (unsigned)((d + 63) / 64));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_gemm_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, BT, d, n, V, ldv, rb, rstride, roff, abort, need));
     return hipGetLastError();
 }
 
@@ -3008,7 +3023,7 @@ hipError_t gemm_f64(const double* X, int64_t ldx, const double* MT, int d, int64
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + 63) / 64), (unsigned)((d + 63) / 64));
     hipLaunchKernelGGL(bz_gemm_kernel<double>, grid, dim3(256), 0, st, X, ldx, nullptr, MT, d, n, V,
-                       (int64_t)d, n, (int64_t)0, (int64_t)0, (const unsigned int*)nullptr);
+                       (int64_t)d, n, (int64_t)0, (int64_t)0, (const unsigned int*)nullptr, (const unsigned int*)nullptr);
     return hipGetLastError();
 }
 

@@ -322,8 +322,9 @@ def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device,
     no host synchronisation) for everything the caller enqueued on its current
     stream before each call -- the lag-sum update still reading the reused v
     buffer, the zeroed accumulators -- and the caller's stream waits for the
-    library's work after it (lgs_imhk itself ends with a synchronisation of its
-    stream, so that wait is free)."""
+    library's work after it.  On a stream set this way lgs_imhk waits only for each
+    block's Klein launch (its flags decide a redo), not for the accept / moments /
+    B z launches behind it: the host enqueues the next step while they run."""
     import torch
     from . import _capi
     st = {"z": torch.zeros((d, n_chains), dtype=torch.int32, device=device),

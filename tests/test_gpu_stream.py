@@ -253,3 +253,61 @@ def test_imhk_ex_lag_sums_with_thinning_across_calls():
         else:
             np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)
     assert np.array_equal(zr.cpu().numpy(), np.concatenate(xs_z, 1)[:, -L:])
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from lgs_amd import _capi
+    _capi.load_library()
+    return _capi
+
+
+def _imhk_carried(capi, on_caller_stream: bool, zmax: int):
+    """lgs_imhk_ex with device pointers: chain states carried in with |z| up to zmax
+    and a log weight no proposal beats, so every kept state is the carried one."""
+    import torch
+    from conftest import golden_R, load_golden
+    g = load_golden("klein_qary128.npz")
+    R, cp, B = golden_R(g)
+    ctx = capi.Context(0)  # fresh: the wider store after a 16-bit overflow is sticky
+    ctx.set_basis(R, cp, B, float(g["sigma"]))
+    d, nc, steps = R.shape[0], 256, 6
+    dev = "cuda:0"
+    rng = np.random.default_rng(zmax)
+    z0 = rng.integers(-zmax, zmax + 1, size=(d, nc)).astype(np.int32)
+    z0[:, 0] = zmax
+    z = torch.from_numpy(z0).to(dev)
+    lw = torch.full((nc,), 1e300, dtype=torch.float64, device=dev)
+    init = torch.ones(nc, dtype=torch.int32, device=dev)
+    acc = torch.zeros(nc, dtype=torch.int64, device=dev)
+    vs = torch.zeros((nc, steps, d), dtype=torch.float64, device=dev)
+    vn2 = torch.zeros((nc, steps), dtype=torch.float64, device=dev)
+    zk = torch.zeros((nc, steps), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream(device=dev)
+    if on_caller_stream:  # lgs_set_stream: the call's early check applies
+        ctx.set_stream(s.cuda_stream)
+    ctx.imhk(5, 0, nc, 1, steps, 1, z, lw, init, acc, v_samples=vs, vnorm2_samples=vn2, zk_samples=zk,
+             zk_index=3, flags=capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR)
+    torch.cuda.synchronize()
+    out = {k: t.cpu().numpy() for k, t in dict(z=z, acc=acc, v=vs, vn2=vn2, zk=zk).items()}
+    ctx.close()
+    return z0, B, out
+
+
+@pytest.mark.parametrize("zmax", [200, 32639, 32700, 40000])
+def test_early_check_equals_synchronised_call(capi, zmax):
+    """lgs_imhk on a caller's stream checks each block's flags right after its abort
+    producers and leaves B z's digit-range replay to the device (gated fp64 launch);
+    the results equal the same call on the library's own stream (host-checked), and
+    v is exactly B z of the carried states -- including |z| beyond the int8 digits
+    (32640..32767: the replay alone; > 32767: also the 16-bit store's redo)."""
+    z0, B, a = _imhk_carried(capi, True, zmax)
+    _, _, b = _imhk_carried(capi, False, zmax)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    assert not a["acc"].any()
+    want = (B.astype(np.int64) @ z0.astype(np.int64)).T  # nc x d
+    for t in range(a["v"].shape[1]):
+        assert np.array_equal(a["v"][:, t, :], want.astype(np.float64)), t
+        assert np.array_equal(a["zk"][:, t], z0[3, :].astype(np.int64)), t
