@@ -211,7 +211,11 @@ def main():
     flags = _capi.LGS_EXACT_ORDER if args.exact_order else 0
     # the timed path is lgs_amd.distributed's StreamingShard: one lgs_imhk call per
     # bench step, lag sums on the device, one all-reduce (tests/test_distributed.py
-    # drives the same class with the oracle over gloo, world 2)
+    # drives the same class with the oracle over gloo, world 2); all of it on one
+    # work stream, which the library then uses as its own (no cross-stream waits)
+    torch.cuda.synchronize()
+    if os.environ.get("LGS_BENCH_DEFAULT_STREAM") != "1":  # (=1: the A/B switch)
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     advance = D.gpu_advance(ctx, seed, first_chain, nc, d, dev, flags=flags, block_steps=T, want_v=not args.no_v,
                             fn_chains=ACF_CHAINS)
     shard = D.StreamingShard(advance, nc, d, binv_row=binv_k, device=dev, lag_chains=ACF_CHAINS, lags=ACF_LAGS,

@@ -318,11 +318,13 @@ def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device,
     functionals ("zk", "vn2") cover the leading ``fn_chains`` chains (0: all; a
     StreamingShard reads its first ``lag_chains``).
 
-    Streams: the library runs on a dedicated torch stream that waits (on the GPU,
-    no host synchronisation) for everything the caller enqueued on its current
-    stream before each call -- the lag-sum update still reading the reused v
-    buffer, the zeroed accumulators -- and the caller's stream waits for the
-    library's work after it.  On a stream set this way lgs_imhk waits only for each
+    Streams: the library runs on the caller's current stream when that is not the
+    null stream at creation (bench.py: one work stream, no cross-stream waits);
+    otherwise on a dedicated torch stream.  A call made from any other current
+    stream makes the library's stream wait (on the GPU, no host synchronisation) for
+    everything enqueued there -- the lag-sum update still reading the reused v
+    buffer, the zeroed accumulators -- and that stream wait for the library's work
+    after it.  On a stream set this way lgs_imhk waits only for each
     block's Klein launch (its flags decide a redo), not for the accept / moments /
     B z launches behind it: the host enqueues the next step while they run."""
     import torch
@@ -335,14 +337,19 @@ def gpu_advance(ctx, seed: int, first_chain: int, n_chains: int, d: int, device,
           "zk": None, "vn2": None}
     fl = flags | _capi.LGS_DEVICE_PTRS | _capi.LGS_COORD_MAJOR
     nfn = n_chains if fn_chains <= 0 else min(int(fn_chains), n_chains)
-    lib_stream = torch.cuda.Stream(device=device)
+    cur = torch.cuda.current_stream(device)
+    lib_stream = cur if cur.cuda_stream else torch.cuda.Stream(device=device)
     ctx.set_stream(lib_stream.cuda_stream)
 
     def _enter():
-        lib_stream.wait_stream(torch.cuda.current_stream(device))
+        cur = torch.cuda.current_stream(device)
+        if cur != lib_stream:
+            lib_stream.wait_stream(cur)
 
     def _leave():
-        torch.cuda.current_stream(device).wait_stream(lib_stream)
+        cur = torch.cuda.current_stream(device)
+        if cur != lib_stream:
+            cur.wait_stream(lib_stream)
 
     lag = {}
 

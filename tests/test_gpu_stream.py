@@ -52,9 +52,10 @@ def test_lag_sums_graph_replay_equals_eager():
         assert np.array_equal(a, b)
 
 
-def _gpu_shard(sync_each: bool, blocks: int = 4):
+def _gpu_shard(sync_each: bool, blocks: int = 4, flags=None, work_stream: bool = False):
     """StreamingShard driven through gpu_advance (lgs_imhk on the library's stream,
-    the lag-sum graph and the thinned Gram on the caller's), C2 q-ary d = 128."""
+    the lag-sum graph and the thinned Gram on the caller's), C2 q-ary d = 128;
+    work_stream: everything on one non-default current stream (as bench.py)."""
     import torch
     from lgs_amd import _capi
     from lgs_amd import distributed as D
@@ -68,7 +69,21 @@ def _gpu_shard(sync_each: bool, blocks: int = 4):
     ctx.set_basis(R, cp, B, sigma)
     dev = torch.device("cuda", 0)
     nc, T = 2048, 16
-    adv = D.gpu_advance(ctx, 31, 0, nc, d, dev, flags=_capi.LGS_WANG_LING, block_steps=T)
+    prev = torch.cuda.current_stream(dev)
+    if work_stream:
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
+    try:
+        return _gpu_shard_run(ctx, D, B, d, dev, nc, T, sync_each, blocks,
+                              _capi.LGS_WANG_LING if flags is None else flags)
+    finally:
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(prev)
+
+
+def _gpu_shard_run(ctx, D, B, d, dev, nc, T, sync_each, blocks, flags):
+    import torch
+    adv = D.gpu_advance(ctx, 31, 0, nc, d, dev, flags=flags, block_steps=T)
     sh = D.StreamingShard(adv, nc, d, binv_row=np.linalg.inv(B)[d - 1], device=dev, lag_chains=512, lags=6,
                           gram_every=2)
     for _ in range(blocks):
@@ -93,6 +108,20 @@ def test_gpu_advance_streams_match_synchronized_run():
         for x, y in zip(xa, xb):
             assert np.array_equal(x, y), k
     assert 0 < int(a["accepts"][0]) < 2048 * 64
+
+
+def test_gpu_advance_on_the_callers_work_stream():
+    """Reference weights (the early check) with the library on the caller's own
+    non-default stream (bench.py's layout: no cross-stream waits) equal the run on
+    the default stream synchronised after every block."""
+    a = _gpu_shard(False, flags=0, work_stream=True)
+    b = _gpu_shard(True, flags=0)
+    assert set(a) == set(b) and "gram" in a
+    for k in a:
+        xa, xb = (a[k], b[k]) if isinstance(a[k], list) else ([a[k]], [b[k]])
+        for x, y in zip(xa, xb):
+            assert np.array_equal(x, y), k
+    assert int(a["accepts"][0]) > 0
 
 
 @pytest.mark.parametrize("cfg", ["C3_ntru512", "C2_qary128"])
