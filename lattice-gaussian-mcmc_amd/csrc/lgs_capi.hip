@@ -661,7 +661,11 @@ int lgs_destroy(lgs_ctx* c) {
 int lgs_set_stream(lgs_ctx* c, void* s) {
     int rc = check_ctx(c, false);
     if (rc) return rc;
-    c->stream = s ? (hipStream_t)s : c->own;
+    const hipStream_t ns = s ? (hipStream_t)s : c->own;
+    // the old stream may still run an early-checked lgs_imhk's later launches, which
+    // read the context's buffers: finish them before another stream reuses those
+    if (ns != c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
+    c->stream = ns;
     return LGS_OK;
 }
 
