@@ -75,7 +75,12 @@ def parse():
     ap.add_argument("--imhk-steps", type=int, default=64, help="IMHK steps per bench step (one lgs_imhk call)")
     ap.add_argument("--no-v", action="store_true", help="skip lattice points (coefficients only)")
     ap.add_argument("--exact-order", action="store_true")
-    ap.add_argument("--cpu-samples", type=int, default=0, help="IMHK proposals for the C-oracle baseline")
+    ap.add_argument("--cpu-samples", type=int, default=0,
+                    help="IMHK proposals for the C-port baseline (0: 512 per core, < 0: skip it)")
+    ap.add_argument("--wl-steps", type=int, default=3,
+                    help="timed bench steps of the Wang-Ling leg after the headline (0: skip)")
+    ap.add_argument("--wl-check-chains", type=int, default=8,
+                    help="chains of the Wang-Ling leg replayed by the C oracle")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--numpy-samples", type=int, default=24, help="Klein samples per process, NumPy baseline")
     ap.add_argument("--no-cpu", action="store_true")
@@ -159,6 +164,54 @@ def load_counters(path, config, bid):
     if bid is None or cnt.get("build_id") != bid:
         return None, rel, "stale"
     return cnt, rel, "current"
+
+
+def wang_ling_leg(args, ctx, D, _capi, lgs_oracle, R, cp, B, sigma, d, nc, T, seed, dev, binv_k):
+    """The headline pipeline (StreamingShard over lgs_imhk_ex: Klein proposals, the
+    certified Wang-Ling accept kernel, moments, B z, lag sums, Gram) with Wang-Ling
+    weights (LGS_WANG_LING), 1 untimed + args.wl_steps timed steps; the first
+    args.wl_check_chains chains replayed by the C oracle (same Philox counters):
+    per-chain accept counts and final states must be equal."""
+    import torch
+    flags = _capi.LGS_WANG_LING | (_capi.LGS_EXACT_ORDER if args.exact_order else 0)
+    adv = D.gpu_advance(ctx, seed, 0, nc, d, dev, flags=flags, block_steps=T, want_v=not args.no_v,
+                        fn_chains=ACF_CHAINS)
+    shard = D.StreamingShard(adv, nc, d, binv_row=binv_k, device=dev, lag_chains=ACF_CHAINS, lags=ACF_LAGS,
+                             gram_every=args.gram_every)
+    ctx.counter(_capi.LGS_COUNTER_ACCEPT_RESOLVED, reset=True)
+    ctx.counter(_capi.LGS_COUNTER_WL_MISMATCH, reset=True)
+    shard.step(T)  # warm-up block (initial draws + 64 steps)
+    torch.cuda.synchronize()
+    acc0 = shard.acc.clone()
+    t0 = time.perf_counter()
+    for _ in range(args.wl_steps):
+        shard.step(T)
+    shard.reduce()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    props = args.wl_steps * nc * T
+    acc = shard.acc.cpu().numpy()
+    acc_timed = int((shard.acc - acc0).sum().item())
+    m = min(args.wl_check_chains, nc)
+    steps_all = (1 + args.wl_steps) * T
+    t1 = time.perf_counter()
+    zo, lwo, acco = lgs_oracle.imhk_parallel(R, cp, B, sigma, m, steps_all, seed=seed, first_step=1,
+                                             mode=lgs_oracle.IMHK_WANG_LING, threads=min(m, cpu_share()))
+    tcpu = time.perf_counter() - t1
+    zg = adv.state["z"][:, :m].cpu().numpy().T
+    same_acc = int(sum(int(acc[c]) == int(acco[c]) for c in range(m)))
+    same_z = int(sum(np.array_equal(zg[c], zo[c]) for c in range(m)))
+    return {"value": round(props / el, 1), "unit": "samples/s", "ms_per_step": round(1e3 * el / args.wl_steps, 3),
+            "steps": args.wl_steps, "imhk_steps_per_step": T, "chains": nc,
+            "acceptance": round(acc_timed / props, 6),
+            "acceptance_gpu_subset": round(float(acc[:m].sum()) / (m * steps_all), 6),
+            "acceptance_cpu_subset": round(float(acco.sum()) / (m * steps_all), 6),
+            "flags_equal_oracle": f"{same_acc}/{m} chains' accept counts and {same_z}/{m} final states equal "
+                                  f"to the C oracle over {steps_all} Wang-Ling steps ({tcpu:.1f} s CPU)",
+            "decisions_at_reference_order_weights": ctx.counter(_capi.LGS_COUNTER_ACCEPT_RESOLVED),
+            "wl_mismatch": ctx.counter(_capi.LGS_COUNTER_WL_MISMATCH),
+            "note": "imhk.py:141-177 with the Wang-Ling weight; the q-panel skip does not apply (every mean "
+                    "enters the weight); not part of `value`"}
 
 
 def main():
@@ -340,33 +393,53 @@ def main():
         gemm = {"kernel": "bz_gemm_kernel" if os.environ.get("LGS_BZ_FP64") == "1" else "bz_i8_kernel",
                 "ms_per_step": round(g_ms / args.steps, 3)}
 
-    # ---- CPU baselines (bounded samples; rank 0 at N=1 only)
+    # ---- Wang-Ling leg (after the headline's timed region; not part of `value`):
+    # the one IMHK mode whose acceptance is not identically 1 (imhk.py:102-124 gives a
+    # constant weight), run through the same StreamingShard pipeline, its acceptance
+    # checked against the C oracle on a chain subset (imhk.py:141-177)
+    wang_ling = None
+    if rank == 0 and world == 1 and args.wl_steps > 0:
+        wang_ling = wang_ling_leg(args, ctx, D, _capi, lgs_oracle, R, cp, B, sigma, d, nc, T, seed, dev, binv_k)
+
+    # ---- CPU baselines (bounded samples; rank 0 at N=1 only).  `value` is the
+    # reference's own path: the NumPy restatement of klein.py:101-220 (the
+    # reference's statements and indexing, one process per core), calibrated at
+    # 1.05x the imported reference's per-core rate on the same C3 basis
+    # (profiles/r03_cpu_baseline_calibration.log); the C port (lgs_oracle.c,
+    # OpenMP) is reported beside it as c_port.
     cpu = None
     if world == 1 and not args.no_cpu:
         threads = args.cpu_threads or cpu_share()
-        n_ch = threads
-        cpu_props = args.cpu_samples or 512 * threads
-        steps_cpu = max(1, cpu_props // n_ch)
-        t1 = time.perf_counter()
-        zc_, lwc, accc = lgs_oracle.imhk_parallel(R, cp, B, sigma, n_ch, steps_cpu, seed=seed,
-                                                  first_step=1, threads=threads)
-        tc = time.perf_counter() - t1
-        props = n_ch * (steps_cpu + 1)  # + the initial draw of every chain
-        cpu = {"value": round(props / tc, 2), "unit": "Klein samples/s", "cores": threads, "kind": "port",
-               "sample": f"C oracle (lgs_oracle.c, OpenMP): {n_ch} IMHK chains x {steps_cpu} steps (+1 initial "
-                         f"draw), same basis, reference-mode weights, {tc:.1f} s wall on {threads} threads",
-               "acceptance": float(accc.sum() / (n_ch * steps_cpu)),
-               "per_core": round(props / tc / threads, 2), "host_cpus": os.cpu_count(),
-               "cpu_model": _cpu_model()}
+        c_port = None
+        if args.cpu_samples >= 0:
+            n_ch = threads
+            cpu_props = args.cpu_samples or 512 * threads
+            steps_cpu = max(1, cpu_props // n_ch)
+            t1 = time.perf_counter()
+            zc_, lwc, accc = lgs_oracle.imhk_parallel(R, cp, B, sigma, n_ch, steps_cpu, seed=seed,
+                                                      first_step=1, threads=threads)
+            tc = time.perf_counter() - t1
+            props = n_ch * (steps_cpu + 1)  # + the initial draw of every chain
+            c_port = {"value": round(props / tc, 2), "unit": "Klein samples/s", "cores": threads, "kind": "port",
+                      "sample": f"C oracle (lgs_oracle.c, OpenMP): {n_ch} IMHK chains x {steps_cpu} steps "
+                                f"(+1 initial draw), same basis, reference-mode weights, {tc:.1f} s wall on "
+                                f"{threads} threads",
+                      "acceptance": float(accc.sum() / (n_ch * steps_cpu)),
+                      "per_core": round(props / tc / threads, 2)}
+        cpu = {"value": None, "unit": "Klein samples/s", "cores": threads, "kind": "reference-restatement",
+               "host_cpus": os.cpu_count(), "cpu_model": _cpu_model(), "c_port": c_port,
+               "acceptance": None if c_port is None else c_port["acceptance"]}
         if args.numpy_samples > 0:
             import lgs_numpy_restatement as NR
             rate, tot, wall = NR.timed_run(R, cp, B, sigma, processes=threads,
                                            samples_per_process=args.numpy_samples, seed=seed)
-            cpu["numpy_restatement"] = {
-                "value": round(rate, 2), "unit": "Klein samples/s", "cores": threads,
-                "per_core": round(rate / threads, 3),
-                "sample": f"{tot} Klein samples of the reference's NumPy loop (klein.py:101-220), "
-                          f"{threads} processes x {args.numpy_samples}, {wall:.1f} s per process"}
+            cpu.update({
+                "value": round(rate, 2), "per_core": round(rate / threads, 3),
+                "sample": f"{tot} Klein samples of the reference's NumPy loop (klein.py:101-220, "
+                          f"oracle/lgs_numpy_restatement.py), {threads} processes x {args.numpy_samples} "
+                          f"samples, one BLAS thread each, {wall:.1f} s per process",
+                "calibration": "restatement / imported reference = 1.051 per core on the same C3 basis and "
+                               "samples (profiles/r03_cpu_baseline_calibration.log)"})
 
     dinfo = ctx.device_info()
     out = {
@@ -391,6 +464,8 @@ def main():
                    "collective": collective},
         "imhk_acceptance": round(acceptance, 6),
         "imhk_acceptance_cpu_reference": None if cpu is None else cpu["acceptance"],
+        # (reference mode: the weight is a constant up to rounding, acceptance 1; the
+        # Wang-Ling leg below carries the acceptance that can differ)
         "parity_check": parity,
         "certificate_redos": {"verified_subpanels": redos, "per_proposal": redos / (args.steps * nc * T)},
         "autocorrelation": acf,
@@ -400,6 +475,7 @@ def main():
         "kernel_ms": {"klein": round(k_ms / max(k_n, 1), 3), "bz": round(g_ms / max(g_n, 1), 3),
                       "accept": round(a_ms / max(a_n, 1), 3), "moments": round(m_ms / max(m_n, 1), 3)},
         "cpu_baseline": cpu,
+        "wang_ling": wang_ling,
         "device": dinfo["name"],
     }
     print(json.dumps(out))

@@ -139,6 +139,9 @@ struct lgs_ctx {
     bool has_Bi8 = false;
     int64_t bd_rows = 0, bd_cols = 0;
     std::vector<BzCall> pending_i8;
+    // an int8 B z whose fp64 replay was enqueued on the device, gated on the digit-range
+    // flag (run_bz device_replay): settle_bz then only clears that flag bit
+    bool i8_dev_replay = false;
     // scratch
     DevBuf Z, LW, V, sel, fsel, cnt, ccnt, flags, stage_a, stage_b, stage_c, stage_d, stage_e,
         stage_f, stage_g, stage_h, stage_i, vs;
@@ -210,7 +213,7 @@ int run_bz_fp64(lgs_ctx* c, const BzCall& b);
 // f0_known: the caller has synchronised and read flag word 0 already (*f0_known).
 int settle_bz(lgs_ctx* c, const unsigned int* f0_known = nullptr) {
     if (!f0_known) HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->pending_i8.empty()) return LGS_OK;
+    if (c->pending_i8.empty() && !c->i8_dev_replay) return LGS_OK;
     {
         unsigned int f0 = 0;
         if (f0_known)
@@ -227,6 +230,7 @@ int settle_bz(lgs_ctx* c, const unsigned int* f0_known = nullptr) {
             HIP_TRY(hipStreamSynchronize(c->stream));
         }
         c->pending_i8.clear();
+        c->i8_dev_replay = false;
     }
     return LGS_OK;
 }
@@ -336,6 +340,7 @@ int finish_or_redo(lgs_ctx* c, bool oz_used, int& zb, bool& redo, bool early = f
     }
     if (!(fw[0] & lgs::kAbortMask)) return finish(c, fw, early);
     c->pending_i8.clear();
+    c->i8_dev_replay = false;
     for (auto& t : c->pending) {  // the aborted attempt's timers are not kept
         c->pool.push_back(t.a);
         c->pool.push_back(t.b);
@@ -535,6 +540,7 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
                                VNP, vn_n));
     if (VN) HIP_TRY(lgs::launch::vnorm2_reduce(VNP, (int)c->d, vn_n, b.rb, b.rstride, b.roff, VN, c->stream, abort));
     if (device_replay) {  // the fp64 replay enqueued now, run only if the digit-range flag is set
+        c->i8_dev_replay = true;
         const unsigned int* need = c->flags.as<unsigned int>();
         HIP_TRY(lgs::launch::bz(b.Z, b.zb, b.ldz, b.sel, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
                                 b.rstride, b.roff, c->stream, abort, need));
@@ -679,6 +685,10 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     if (!(sigma > 0) || !std::isfinite(sigma))
         return fail(LGS_ERR_INVALID, "Standard deviation must be positive, got %g", sigma);
     if (precision <= 0) return fail(LGS_ERR_INVALID, "precision must be positive");
+    // an early-checked lgs_imhk / an asynchronous lgs_gram may still run on the
+    // context's stream and read R, BT, the digit planes, records, EMAX: the blocking
+    // copies below are not ordered after a non-blocking stream's work
+    HIP_TRY(hipStreamSynchronize(c->stream));
     const int PB = c->panel;
     const size_t dd = (size_t)d;
     // per-coordinate parameters (klein.py:195-211, 255-263)
@@ -1376,6 +1386,7 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
         aa.acc_step = accs ? accs + t0 : nullptr;
         aa.acc_ld = n_steps;
         aa.abort = fl;
+        aa.state_init = init;  // the step each chain's state was drawn at (certified Wang-Ling replays)
         if (certw) {  // certified Wang-Ling decisions (imhk_accept_cert_kernel)
             aa.LWE = c->LWE.as<double>();
             aa.emax = c->EMAX.as<unsigned long long>();
@@ -1389,8 +1400,9 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             aa.zs_cm = cm ? 1 : 0;
             aa.flagw = fl;
             // test hook: widened bounds force the recomputation path on many decisions
+            // (clamped to >= 1: a smaller scale would shrink the bounds and void the certificate)
             const char* bs = getenv("LGS_TEST_WL_BOUND_SCALE");
-            aa.bscale = bs ? atof(bs) : 1.0;
+            aa.bscale = bs ? std::max(1.0, atof(bs)) : 1.0;
         }
         {
             Scope s(c, 2);
@@ -1419,8 +1431,12 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             const int64_t nq = nc * kb;
             if (v_samples) {  // rows (chain, first_keep + k) of the n_chains x n_keep x d output,
                               // read straight from the proposal store through the selections
+                // the fp64 replay of a digit-range overflow runs on the device, before its
+                // consumers, when the host cannot replay it first: the early check, and the
+                // lag sums below, which read ||v||^2 inside this call
+                const bool dev_replay = early || (lag && lag->lag_v_sums && vnorm2_samples);
                 if ((rc = run_bz(c, c->Z.p, zb, ldzb, nq, v_samples, kb, n_keep, first_keep,
-                                 c->sel.as<int64_t>(), true, fl, vnorm2_samples, fn_chains * kb, early)))
+                                 c->sel.as<int64_t>(), true, fl, vnorm2_samples, fn_chains * kb, dev_replay)))
                     return rc;
             }
             if (zk_samples)  // (the leading fn_chains chains' kept states: q < fn_chains * kb)
@@ -1997,6 +2013,7 @@ int lgs_set_decoder(lgs_ctx* c, const double* Q, const double* Binv) {
     if (rc) return rc;
     const int64_t d = c->d;
     const size_t bytes = (size_t)d * d * 8;
+    HIP_TRY(hipStreamSynchronize(c->stream));  // (as lgs_set_basis: in-flight work may read the buffers)
     if (Q) {
         if ((rc = c->DQ.reserve(bytes))) return rc;
         HIP_TRY(hipMemcpy(c->DQ.p, Q, bytes, hipMemcpyHostToDevice));  // gemm_f64 reads Q[c][r]

@@ -192,7 +192,16 @@ struct AcceptArgs {
     int zs_cm;
     unsigned int* flagw;    // the context's flag words (kFlagWordAcceptResolved, kFlagWordWLMismatch)
     double bscale;          // bounds x bscale (1; a test hook widens them to force recomputations)
+    // nullable: the chains' state_init words (lgs.h): >= kInitStep0 = the state is the
+    // chain's draw at counter step (word - kInitStep0), so a carried-in state's weight is
+    // recomputed with its own uniforms; 1 = initialised, step unknown.  Updated for the
+    // chains whose state changes in the block.
+    int32_t* state_init;
 };
+constexpr int32_t kInitStep0 = 2;
+__host__ __device__ inline int32_t init_code(uint32_t step) {
+    return step <= 0x7fffffffu - (uint32_t)kInitStep0 ? (int32_t)step + kInitStep0 : 1;
+}
 
 // Per-series statistics (lgs_diag.hip series_stats_kernel).  Series s starts at
 // x + (s / gsize) * gstride + (s % gsize) * sstride, time step t at + t * tstride.

@@ -166,7 +166,11 @@ struct RecRegs {
 #endif
     __device__ __forceinline__ double operator[](int k) const { return v[k]; }
 };
-__device__ __forceinline__ RecRegs load_rec(lds_cdptr rec) {
+struct NoMid {
+    __device__ __forceinline__ void operator()() const {}
+};
+template <typename MID = NoMid>
+__device__ __forceinline__ RecRegs load_rec(lds_cdptr rec, MID mid = MID{}) {
     typedef double d2v __attribute__((ext_vector_type(2)));
     using lds_d2p = const __attribute__((address_space(3))) d2v*;
     RecRegs r;
@@ -176,6 +180,7 @@ __device__ __forceinline__ RecRegs load_rec(lds_cdptr rec) {
         r.v[2 * k] = t[0];
         r.v[2 * k + 1] = t[1];
     }
+    mid();
 #ifdef LGS_CAP_RI_PRE
     r.ri = load_cap_ri();
 #endif
@@ -1411,7 +1416,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
                     const lds_cdptr rec = (lds_cdptr)rec_lds + (i - (p_hi - 32)) * kRecStride;
                     static_assert(kSzCa == 21 && kSzCb == 22 && kRecCp == 23 && kRecIrii == 24, "record layout");
+#ifdef LGS_DBG1  // hazard reconstruction: the uniform drawn under the record reads, unused
+                    const RecRegs rr = load_rec(rec, [&]() { (void)rs.u((uint32_t)(d - 1 - i)); });
+#else
                     const RecRegs rr = load_rec(rec);
+#endif
                     const double mu = (rr[kRecCp] - acc[15]) * rr[kRecIrii];
                     LGS_DC_T(t_sz0);
                     bool un;
@@ -1776,6 +1785,7 @@ __global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
     a.accepts[c] += acc;
     a.final_sel[c] = cur;
     if (a.cnt_carry) a.cnt_carry[c] = carry;
+    if (a.state_init && cur >= 0) a.state_init[c] = init_code(a.step0 + (uint32_t)(cur % a.T));
 }
 
 // ------------------------------------------------- certified Wang-Ling decisions
@@ -1785,7 +1795,13 @@ __global__ __launch_bounds__(256) void imhk_accept_kernel(const AcceptArgs a) {
 // bounds; otherwise the wave recomputes both weights in the reference's order
 // (wl_exact_wave) and decides at them -- the decision klein_exact_kernel's weights
 // give.  Chain states carried into a block have the bound *emax (the context's
-// running maximum over its Wang-Ling draws).
+// running maximum over its Wang-Ling draws); one that has to be recomputed is
+// replayed with its own counters when its state_init word records the step it was
+// drawn at (the chain's draws are counter-addressed, so the replay is the
+// reference-order weight of that draw, checked to reproduce its z), else with step
+// 0's uniforms (they only select SampleZ's rare table-walk path, whose normaliser
+// agrees to ~1e-13) and a residual bound 1e-12 (1 + |lw|).  Certification covers
+// states drawn in this context since its last lgs_set_basis (EMAX is reset there).
 
 __device__ __forceinline__ double readlane_f64(double v, int k) {
     const long long b = __double_as_longlong(v);
@@ -1902,6 +1918,7 @@ __global__ __launch_bounds__(64) void imhk_accept_cert_kernel(const AcceptArgs a
     const bool live = c < a.nc;
     double lw_x = live ? a.lw_state[c] : 0.0;
     double e_x = a.bscale * __longlong_as_double((long long)*(const volatile unsigned long long*)a.emax);
+    const int32_t sinit = live && a.state_init ? a.state_init[c] : 1;  // the carried state's draw
     int64_t cur = -1;
     int64_t acc = 0;
     int64_t keep = 0;
@@ -1925,6 +1942,7 @@ __global__ __launch_bounds__(64) void imhk_accept_cert_kernel(const AcceptArgs a
             const double eyL = readlane_f64(e_y, L), exL = readlane_f64(e_x, L);
             const int64_t curL = ((int64_t)__builtin_amdgcn_readlane((int)(cur >> 32), L) << 32) |
                                  (uint32_t)__builtin_amdgcn_readlane((int)cur, L);
+            const int32_t sinitL = __builtin_amdgcn_readlane(sinit, L);
             double ly = 0.0, lx = 0.0;
             if (eyL != 0.0)
                 ly = wl_exact_wave(ka, a.RT, (const char*)a.Zst + (cL * a.T + t) * a.zb, a.zb, a.ldz,
@@ -1933,12 +1951,15 @@ __global__ __launch_bounds__(64) void imhk_accept_cert_kernel(const AcceptArgs a
                 if (curL >= 0)  // an earlier proposal of this block
                     lx = wl_exact_wave(ka, a.RT, (const char*)a.Zst + curL * a.zb, a.zb, a.ldz,
                                        a.step0 + (uint32_t)(curL % a.T), chL, true, bad);
-                else  // the state carried in (its counters are not known: the uniforms only
-                      // select the rare table-walk path, whose normaliser agrees to ~1e-13)
+                else  // the state carried in: replayed at its own step when state_init has it
                     lx = wl_exact_wave(ka, a.RT,
                                        (const char*)a.zs + (a.zs_cm ? cL : cL * ka.d) * a.ob, a.ob,
-                                       a.zs_cm ? a.nc : 1, 0u, chL, false, bad);
+                                       a.zs_cm ? a.nc : 1,
+                                       sinitL >= kInitStep0 ? (uint32_t)(sinitL - kInitStep0) : 0u, chL,
+                                       sinitL >= kInitStep0, bad);
             }
+            // a carried state replayed without its counters keeps a residual bound
+            const bool resid = exL != 0.0 && curL < 0 && sinitL < kInitStep0;
             if (lane == L) {
                 if (eyL != 0.0) {
                     lw_y = ly;
@@ -1948,7 +1969,7 @@ __global__ __launch_bounds__(64) void imhk_accept_cert_kernel(const AcceptArgs a
                 }
                 if (exL != 0.0) {
                     lw_x = lx;
-                    e_x = 0.0;
+                    e_x = resid ? 1e-12 * (1.0 + fabs(lx)) : 0.0;
                     if (cur >= 0) {
                         a.LWx[cur] = lx;
                         a.LWE[cur] = 0.0;
@@ -1985,6 +2006,7 @@ __global__ __launch_bounds__(64) void imhk_accept_cert_kernel(const AcceptArgs a
     a.accepts[c] += acc;
     a.final_sel[c] = cur;
     if (a.cnt_carry) a.cnt_carry[c] = carry;
+    if (a.state_init && cur >= 0) a.state_init[c] = init_code(a.step0 + (uint32_t)(cur % a.T));
 }
 
 // ------------------------------------------------------------ moments
@@ -2233,7 +2255,7 @@ __global__ __launch_bounds__(256) void init_apply_kernel(const ZT* __restrict__ 
             zs[(size_t)c * d + i] = v;
     }
     lws[c] = LW[c];
-    init[c] = 1;
+    init[c] = kInitStep0;  // the draw at counter step 0
 }
 
 // Z[coord][p] (ld ldz) -> out[p][coord] (row-major n x d), 64x64 tiles via LDS.

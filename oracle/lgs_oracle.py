@@ -19,7 +19,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "liblgs_oracle.so")
+# LGS_ORACLE_LIB: another build of the same source (the ASan/UBSan one, `make sanitize`)
+_LIB_PATH = os.environ.get("LGS_ORACLE_LIB") or os.path.join(_HERE, "_build", "liblgs_oracle.so")
 _lib = None
 
 RNG_MT = 0
