@@ -867,6 +867,16 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
             all = r[0] != 0.0 && (int)r[2] == lgs::kSzSmall && r[7] == 0.0;
         }
         for (int64_t i = top - 16; i < top; ++i) crec[i * lgs::kRecStride + lgs::kRecSpec] = all ? 1.0 : 0.0;
+        if (all) continue;
+        // 2: every coordinate of the sub-panel capped with sigma >= 360 (the near field
+        // then skips the per-coordinate kind dispatch, klein_mfma_kernel)
+        bool cap = true;
+        for (int64_t i = top - 16; i < top && cap; ++i) {
+            const double* r = crec.data() + i * lgs::kRecStride;
+            cap = r[0] != 0.0 && (int)r[2] == lgs::kSzCapped && r[7] == 1.0;
+        }
+        if (cap)
+            for (int64_t i = top - 16; i < top; ++i) crec[i * lgs::kRecStride + lgs::kRecSpec] = 2.0;
     }
     // q-panel skip (klein_mfma_kernel, reference mode): for a 32-row panel whose rows
     // all lie in speculative sub-panels, the largest ||z_W||_2^2 (W = coordinates
@@ -882,7 +892,7 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     bool any_q = false;
     if (!(flags & LGS_BASIS_LINEAR_PROBS)) {
         std::vector<char> inW(dd);
-        for (size_t i = 0; i < dd; ++i) inW[i] = crec[i * lgs::kRecStride + lgs::kRecSpec] == 0.0;
+        for (size_t i = 0; i < dd; ++i) inW[i] = crec[i * lgs::kRecStride + lgs::kRecSpec] != 1.0;
         const double g = 1.1 * (double)d * std::ldexp(1.0, -53);
         for (int64_t pk = 0; pk < npan32; ++pk) {
             const int64_t p_hi = d - 32 * pk;

@@ -315,6 +315,57 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
     return zi;
 }
 
+// The rolled near field's running-sum update acc[k + 1] = fma(r, z, acc[k]) (k
+// descending, in place).  Left to itself the compiler selects the two-address
+// v_fmac_f64 (dst = addend): each result then lands in the register of acc[k], and
+// the loop's back edge needs 15 v_mov_b64 per coordinate to shift the sums back.
+// The three-address v_fma_f64 writes acc[k + 1]'s own register: no moves, the same
+// fused operations (round 5: Klein 2.507 / 2.513 -> 2.443 / 2.456 ms per 2^18 C3
+// samples, identical outputs, profiles/r05b_kb.log).  LGS_NEAR_FMA_PLAIN: fma().
+__device__ __forceinline__ double fma_shift(double a, double b, double c) {
+#ifndef LGS_NEAR_FMA_PLAIN
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return fma(a, b, c);
+#endif
+}
+
+// decide_coord_rec for a coordinate of a sub-panel the host flagged all capped with
+// sigma >= 360 (kRecSpec == 2: kind kSzCapped, q[7] == 1, sigma_i != 0): the same
+// decision and weight bookkeeping without the per-coordinate kind dispatch (its
+// vector -> scalar turnarounds sit on the near field's dependency chain).
+template <bool WL, typename TP>
+__device__ __forceinline__ double decide_capped_rec(const KleinArgs& a, int i, double mu, lds_cdptr rec,
+                                                    const RecRegs& rr, CoordStream& rs, double& lw,
+                                                    unsigned int& flags, TP etab, double dmu, bool& amb,
+                                                    double& eb, double& tb) {
+    amb = false;
+    if (!isfinite(mu)) {
+        flags |= kFlagNonFinite;
+        return 0.0;
+    }
+    QHead qh;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) qh.v[k] = rr[k];
+    const double u = rs.u((uint32_t)(a.d - 1 - i));
+    SzPair r;
+    r.ln = 0.0;
+    r.z = sample_z_capped<true>(mu, u, qh, RecView{rr}, WL, r.ln, dmu);
+    double ln = 0.0;
+    const double zi = sz_finish<true>(r, mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, ln, dmu, amb);
+    if (WL) {
+        lw += ln;
+        tb += fabs(ln);
+        eb += amb ? 0.0 : wl_bound_generic(ln, qh.v[1], wl_window_hw(qh.v[6]), dmu);
+    } else {
+        const double t = ref_weight(zi, mu, rr[kRecRos], rr[kRecIsr], rr[kRecLterm]);
+        lw += amb ? 0.0 : t;
+    }
+    return zi;
+}
+
 // z is an exact fp64 integer; int64 stores convert it, narrower stores flag
 // values outside their range.
 template <typename ZT>
@@ -1406,6 +1457,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
 #pragma unroll
                 for (int j = 0; j < 8; ++j) hp[j] = 0u;
                 int flm = 0;
+#ifdef LGS_CAP_SP
+                // the whole sub-panel is capped with sigma >= 360 (host flag kRecSpec == 2)
+                const int capsp = !LIBM && rows16 == 16 &&
+                                  __builtin_amdgcn_readfirstlane((int)((lds_cdptr)rec_lds)[(top - 1 - (p_hi - 32)) * kRecStride + kRecSpec]) == 2;
+#endif
                 bool snz = false;  // (OZ) a nonzero z in this sub-panel, this lane
                 double zsq = 0.0;  // (q-panel skip) sum z^2 of this sub-panel, this lane
 #ifndef LGS_NEAR_UNROLL  // coordinates per loop iteration (the running sums shift by one per step)
@@ -1413,6 +1469,9 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
 #endif
 #pragma unroll LGS_NEAR_UNROLL
                 for (int s = 0; s < rows16; ++s) {
+#ifdef LGS_DIAG_STEP  // diagnostic builds only: phases of a near-field step (lgs_diag_cycles [3] [4] [5])
+                    LGS_DC_T(t_stepA);
+#endif
                     const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
                     const lds_cdptr rec = (lds_cdptr)rec_lds + (i - (p_hi - 32)) * kRecStride;
                     static_assert(kSzCa == 21 && kSzCb == 22 && kRecCp == 23 && kRecIrii == 24, "record layout");
@@ -1424,17 +1483,31 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     const double mu = (rr[kRecCp] - acc[15]) * rr[kRecIrii];
                     LGS_DC_T(t_sz0);
                     bool un;
+#ifdef LGS_CAP_SP
+                    int cf = __builtin_amdgcn_readfirstlane(capsp);
+                    asm volatile("" : "+s"(cf));  // a scalar test per step (no loop unswitching: one copy of the loop)
+                    const double zi = cf ? decide_capped_rec<WL>(a, i, mu, rec, rr, rs, lw, flags, etab_s,
+                                                                 cert_dmu(rr[kSzCa], rr[kSzCb], a.z1cap, mu), un, eb, tb)
+                                         : decide_coord_rec<WL, true, LIBM>(
+                                               a, i, mu, rec, rr, rs, lw, flags, etab_s,
+                                               cert_dmu(rr[kSzCa], coarse ? rec[kRecCbC] : rr[kSzCb], a.z1cap, mu), un,
+                                               eb, tb);
+#else
                     const double zi = decide_coord_rec<WL, true, LIBM>(
                         a, i, mu, rec, rr, rs, lw, flags, etab_s,
                         cert_dmu(rr[kSzCa], coarse ? rec[kRecCbC] : rr[kSzCb], a.z1cap, mu), un, eb, tb);
+#endif
                     flm |= un ? (1 << s) : 0;
-#ifdef LGS_DIAG_CYCLES
+#if defined(LGS_DIAG_CYCLES) && !defined(LGS_DIAG_STEP)
                     {
                         LGS_DC_T(t_sz1);
                         const int kind = (int)rec[2] & 7;
                         LGS_DC_ADD(3 + kind, t_sz1 - t_sz0);
                         LGS_DC_ADD(8 + kind, 1);
                     }
+#endif
+#ifdef LGS_DIAG_STEP
+                    LGS_DC_T(t_stepC);
 #endif
                     // stores: v_cvt_i32_f64 saturates, so no clamps -- a value beyond the
                     // int16 history's range (or a 16-bit store's) flags kFlagOverflow16 and
@@ -1467,8 +1540,19 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     // it and its reload's vmcnt(0) waited for every coordinate's stores
                     if (!hblock) z1e += fabs(zi);
 #pragma unroll
-                    for (int k = 14; k >= 0; --k) acc[k + 1] = fma(rr[kRecRs + 14 - k], zi, acc[k]);
+                    for (int k = 14; k >= 0; --k) acc[k + 1] = fma_shift(rr[kRecRs + 14 - k], zi, acc[k]);
                     acc[0] = 0.0;
+#ifdef LGS_DIAG_STEP
+                    {
+                        LGS_DC_T(t_stepD);
+                        LGS_DC_ADD(3, t_sz0 - t_stepA);  // record batch + mean
+                        LGS_DC_ADD(4, t_stepC - t_sz0);  // decision (kind dispatch, Philox, SampleZ, weight)
+                        LGS_DC_ADD(5, t_stepD - t_stepC);  // stores, history packing, bookkeeping, 15 FMAs
+                        LGS_DC_ADD(8, 1);
+                        LGS_DC_ADD(9, 1);
+                        LGS_DC_ADD(10, 1);
+                    }
+#endif
                 }
                 if constexpr (OZ) {
                     if (hblock) {

@@ -312,14 +312,24 @@ def _imhk_carried(capi, on_caller_stream: bool, zmax: int):
     vs = torch.zeros((nc, steps, d), dtype=torch.float64, device=dev)
     vn2 = torch.zeros((nc, steps), dtype=torch.float64, device=dev)
     zk = torch.zeros((nc, steps), dtype=torch.int64, device=dev)
+    # lag sums continued inside the call: they read ||v||^2 before the call returns, so
+    # a digit-range replay of B z must reach them (on the library's own
+    # stream it used to be a host replay after them)
+    L = 3
+    zr = torch.zeros((nc, L), dtype=torch.int64, device=dev)
+    zsum = torch.zeros(L + 2, dtype=torch.int64, device=dev)
+    vr = torch.zeros((nc, L), dtype=torch.float64, device=dev)
+    vsum = torch.zeros(L + 2, dtype=torch.float64, device=dev)
     torch.cuda.synchronize()
     s = torch.cuda.Stream(device=dev)
     if on_caller_stream:  # lgs_set_stream: the call's early check applies
         ctx.set_stream(s.cuda_stream)
     ctx.imhk(5, 0, nc, 1, steps, 1, z, lw, init, acc, v_samples=vs, vnorm2_samples=vn2, zk_samples=zk,
-             zk_index=3, flags=capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR)
+             zk_index=3, flags=capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR,
+             lag=(L, zr, zsum, vr, vsum, 1e-6))
     torch.cuda.synchronize()
-    out = {k: t.cpu().numpy() for k, t in dict(z=z, acc=acc, v=vs, vn2=vn2, zk=zk).items()}
+    out = {k: t.cpu().numpy() for k, t in dict(z=z, acc=acc, v=vs, vn2=vn2, zk=zk, zsum=zsum, vsum=vsum,
+                                                 zr=zr, vr=vr).items()}
     ctx.close()
     return z0, B, out
 
@@ -337,6 +347,21 @@ def test_early_check_equals_synchronised_call(capi, zmax):
         assert np.array_equal(a[k], b[k]), k
     assert not a["acc"].any()
     want = (B.astype(np.int64) @ z0.astype(np.int64)).T  # nc x d
+    # ||v||^2 reaches ~1e20 at |z| ~ 32639 (beyond 2^53: fp64 sums in another order than
+    # numpy's), so against numpy to rounding; the early-checked and host-checked calls
+    # above are equal bit for bit
+    n2 = (want.astype(np.float64) ** 2).sum(1)
     for t in range(a["v"].shape[1]):
         assert np.array_equal(a["v"][:, t, :], want.astype(np.float64)), t
         assert np.array_equal(a["zk"][:, t], z0[3, :].astype(np.int64)), t
+        np.testing.assert_allclose(a["vn2"][:, t], n2, rtol=1e-13, atol=0)
+    # the lag sums of the constant series x_t = 1e-6 ||v||^2 (and z_3) over the 6 steps
+    L, n = len(a["vsum"]) - 2, a["v"].shape[1]
+    for xs, got, exact in ((np.repeat(z0[3, :].astype(np.int64)[:, None], n, 1), a["zsum"], True),
+                           (np.repeat((n2 * 1e-6)[:, None], n, 1), a["vsum"], False)):
+        w = [sum((xs[:, t] * xs[:, t - k]).sum() for t in range(k, n)) for k in range(L + 1)] + [xs.sum()]
+        w = np.array(w, dtype=xs.dtype)
+        if exact:
+            assert np.array_equal(got, w)
+        else:
+            np.testing.assert_allclose(got, w, rtol=1e-12, atol=0)
