@@ -859,6 +859,10 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
         std::copy(rsv.data() + i * 15, rsv.data() + i * 15 + 15, r + lgs::kRecRs);
         r[lgs::kRecScale] = rscale[i];
         r[lgs::kRecCbC] = cbc[i];
+        const int kind = (int)r[2];
+        r[lgs::kRecDisp] = r[0] != 0.0 && kind == lgs::kSzSmall && r[7] == 0.0   ? 0.0
+                           : r[0] != 0.0 && kind == lgs::kSzCapped && r[7] == 1.0 ? 1.0
+                                                                                    : 2.0;
     }
     for (int64_t top = d; top >= 16; top -= 16) {  // whole 16-row sub-panels (top = d - 16 sp)
         bool all = true;

@@ -93,8 +93,11 @@ __device__ __forceinline__ double accept_uniform(uint64_t seed, uint32_t step, u
 template <bool OPAQUE = true>
 struct CoordStreamT {
     uint32_t k0, k1, step, chain;
-    uint32_t pair;  // cached pair index (0xffffffff = none)
+    uint32_t pair;  // cached pair index (0xffffffff = none); LGS_PHILOX2 (OPAQUE): cached quad index
     U4 w;
+#ifdef LGS_PHILOX2
+    U4 w2;  // the quad's second pair
+#endif
     __device__ __forceinline__ void init(uint64_t seed, uint32_t step_, uint32_t chain_) {
         k0 = (uint32_t)seed;
         k1 = (uint32_t)(seed >> 32);
@@ -109,6 +112,21 @@ struct CoordStreamT {
         hh *= 0x2C1B3C6Du;
         hh ^= hh >> 12;
         return (double)hh * 0x1p-32;
+#endif
+#ifdef LGS_PHILOX2
+        // the Klein kernels' wave-uniform slots: the two Philox blocks of a quad of
+        // slots (4 coordinates) computed together -- two independent 10-round chains
+        // the scheduler interleaves -- behind a scalar test (the cache key is uniform)
+        if constexpr (OPAQUE) {
+            const uint32_t q = __builtin_amdgcn_readfirstlane(slot >> 2);
+            if (q != __builtin_amdgcn_readfirstlane(pair)) {
+                w = philox4x32_10<true>(2 * q, step, chain, kTagCoord, k0, k1);
+                w2 = philox4x32_10<true>(2 * q + 1, step, chain, kTagCoord, k0, k1);
+                pair = q;
+            }
+            const U4 ww = (slot & 2u) ? w2 : w;
+            return (slot & 1u) ? u53(ww.z, ww.w) : u53(ww.x, ww.y);
+        }
 #endif
         const uint32_t p = slot >> 1;
         if (p != pair) {
@@ -812,6 +830,12 @@ __device__ __constant__ double kCapCoef[36] = {
     -0.8188084361376584, 4.787814391235978, -17.187235185827564, 42.14891487326897, -68.64189227692192,
     71.76515059941498, -43.593212219926436, 11.853485934431038};
 constexpr int kCapE = 0, kCapG = 11, kCapRI = 23;
+// kCapCoef[kCapRI ..] as compile-time constants (LGS_CAP_IMM)
+constexpr double kCapRIImm[13] = {0.8862269447150851, 0.23200895985592382, 0.1278390124627034,
+                                  0.07920907048159789, 0.16780265291085433, -0.8188084361376584,
+                                  4.787814391235978, -17.187235185827564, 42.14891487326897,
+                                  -68.64189227692192, 71.76515059941498, -43.593212219926436,
+                                  11.853485934431038};
 __device__ __forceinline__ cdptr cap_coef() {
     cdptr p = (cdptr)kCapCoef;
     asm volatile("" : "+s"(p));
@@ -996,7 +1020,20 @@ __device__ __forceinline__ double sample_z_capped(double mu, double u, const QHe
     // continuous quantile x = m + sigma sqrt(2) erfinv(v): erfinv(v) = v R(v^2)
     const cdptr cf = cap_coef();
     const double v = fmin(fmax((target + base) * h.v[4], -0.8485), 0.8485);
+#ifdef LGS_CAP_IMM
+    // the erfinv coefficients as scalar immediates (s_mov) at the use: no scalar-memory
+    // round trip on the decision's dependency chain
+    CapRI rim;
+#pragma unroll
+    for (int k = 0; k < 13; ++k) {
+        rim.c[k] = kCapRIImm[k];
+        asm volatile("" : "+s"(rim.c[k]));
+    }
+    (void)cf;
+    const double xg = fma(h.v[5] * v, poly_h2<13>(rim.c, v * v), m);
+#else
     const double xg = fma(h.v[5] * v, ri ? poly_h2<13>(ri->c, v * v) : poly_estrin_p<13>(cf + kCapRI, v * v), m);
+#endif
 #ifdef LGS_DIAG_CAP_GUESS  // diagnostic builds only (NOT bit-exact): cost probe, decision = the guess
     return c + fmin(fmax(ceil(xg - 0.5), -500.0), 500.0);
 #endif
@@ -1041,8 +1078,13 @@ __device__ __forceinline__ double sample_z_capped(double mu, double u, const QHe
             atomicMax(&lgs_diag_capq[7], (unsigned long long)(dmu * 1e15));
         }
 #endif
+#ifdef LGS_CAP_BRANCHLESS  // every condition evaluated: straight-line compares, no exec-masked branch
+        const bool fast = (xs - fl > tol) & (fl + 1.0 - xs > tol) & (fl >= -501.0) & (fl <= 499.0) &
+                          (fabs(v) < 0.848) & (!CERT | (fabs(m) + 1.01 * dmu < 0.5));
+#else
         const bool fast = xs - fl > tol && fl + 1.0 - xs > tol && fl >= -501.0 && fl <= 499.0 &&
                           fabs(v) < 0.848 && (!CERT || fabs(m) + 1.01 * dmu < 0.5);
+#endif
         // a wave-uniform branch: the evaluation below must not be if-converted into
         // straight-line code that every wave runs
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(!fast) == 0, 1)) {

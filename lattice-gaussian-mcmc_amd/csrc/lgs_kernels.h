@@ -50,9 +50,13 @@ constexpr int kSzcStride = 24;
 // Staged into LDS once per 32-row panel by klein_mfma_kernel.
 constexpr int kRecCp = kSzUsed, kRecIrii = kSzUsed + 1, kRecRos = kSzUsed + 2,
               kRecIsr = kSzUsed + 3, kRecLterm = kSzUsed + 4, kRecRs = kSzUsed + 5;
+// SampleZ dispatch code of the coordinate (host): 0.0 = small kind with one dominant
+// window point possible (q[7] == 0), 1.0 = capped kind with sigma >= 360 (q[7] == 1),
+// 2.0 = anything else (sigma_i == 0 included); inside the hot record batch
+constexpr int kRecDisp = kRecRs + 15;
 // int8-digit far field (klein_mfma_kernel OZ): row scale 2^E_i of the
 // coordinate's row over its panel's far columns
-constexpr int kRecScale = kRecRs + 15;
+constexpr int kRecScale = kRecRs + 16;
 // 1.0 when the coordinate's 16-row sub-panel is whole and all its coordinates are
 // of the small kind with one dominant window point possible (q[7] == 0): the
 // sub-panel is then decided speculatively in parallel (klein_mfma_kernel)
@@ -60,7 +64,7 @@ constexpr int kRecSpec = kRecScale + 1;
 // Cb of the certificate for a mean whose far field used only the 3 most significant
 // R digits (reference mode, panels of two speculative sub-panels: klein_mfma_kernel)
 constexpr int kRecCbC = kRecScale + 2;
-constexpr int kRecStride = kRecRs + 18;  // 46: 368 bytes, 16-byte multiple
+constexpr int kRecStride = kRecRs + 20;  // 48: 384 bytes, 16-byte multiple
 static_assert(kRecCbC < kRecStride, "record layout");
 constexpr int kOzCoarse = 4;  // R digits of the far field in coarse panels
 // int8-digit far field layout: per 32-row panel pk >= 1 (K = 32 pk far columns,

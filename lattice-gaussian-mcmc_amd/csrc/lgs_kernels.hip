@@ -254,9 +254,17 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         double ln = 0.0;
         double ebf = 0.0;  // (WL) the fast decision's weight bound
         // the kind and its flag are the same in every lane: scalar branches
+#ifdef LGS_DISP_CODE
+        // the host's dispatch code (kRecDisp): one scalar read of its high word (0 for
+        // 0.0, 0x3ff00000 for 1.0) instead of converting the kind and testing q[7]
+        const int dsp = __builtin_amdgcn_readfirstlane((int)(__double_as_longlong(rr[kRecDisp]) >> 32));
+        const bool small_fast = dsp == 0, capped1 = dsp == 0x3ff00000;
+#else
         const int kind = __builtin_amdgcn_readfirstlane((int)qh.v[2]);
         const int q7 = __builtin_amdgcn_readfirstlane(qh.v[7] == 0.0 ? 0 : (qh.v[7] == 1.0 ? 1 : 2));
-        if (CERT && kind == kSzSmall && q7 == 0) {
+        const bool small_fast = kind == kSzSmall && q7 == 0, capped1 = kind == kSzCapped && q7 == 1;
+#endif
+        if (CERT && small_fast) {
             // the heaviest window point is rint(mu) (d1 = |mu - rint(mu)| < 1/2 unless a
             // tie, which fails the test); every other point lies >= 1 - d1 from mu, so
             // its log-weight is below the top one by >= is^2 (1 - 2 d1) / 2 -- a lower
@@ -276,7 +284,7 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
             const double u = rs.u((uint32_t)(a.d - 1 - i));
             SzPair r;
 #ifdef LGS_DIAG_NO_GENERIC  // diagnostic builds only: cost of the generic call sites (NOT bit-exact)
-            if (kind == kSzCapped && q7 == 1) {
+            if (capped1) {
                 r = sample_z_capped_leaf<CERT>(mu, u, rec, WL, dmu);
                 amb = CERT && (__builtin_isnan(r.z) || __builtin_isnan(r.ln));
                 zi = __builtin_isnan(r.z) ? rint(mu) : r.z;
@@ -288,7 +296,7 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
 #endif
             {
 #ifndef LGS_NO_CAPPED_POLY
-            if (kind == kSzCapped && q7 == 1) {  // sigma >= 360: the streamlined capped decision
+            if (capped1) {  // sigma >= 360: the streamlined capped decision
                 r.ln = 0.0;
 #ifdef LGS_CAP_RI_PRE
                 r.z = sample_z_capped<CERT>(mu, u, qh, RecView{rr}, WL, r.ln, dmu, &rr.ri);
@@ -1475,7 +1483,10 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     const int i = __builtin_amdgcn_readfirstlane(top - 1 - s);
                     const lds_cdptr rec = (lds_cdptr)rec_lds + (i - (p_hi - 32)) * kRecStride;
                     static_assert(kSzCa == 21 && kSzCb == 22 && kRecCp == 23 && kRecIrii == 24, "record layout");
-#ifdef LGS_DBG1  // hazard reconstruction: the uniform drawn under the record reads, unused
+#if defined(LGS_DBG1) || defined(LGS_PHILOX_TOP)
+                    // (LGS_DBG1: the round-4 hazard reconstruction; LGS_PHILOX_TOP:
+                    // the same placement as an optimisation) the coordinate's Philox block drawn
+                    // under the record's LDS reads, off the decision's dependency chain
                     const RecRegs rr = load_rec(rec, [&]() { (void)rs.u((uint32_t)(d - 1 - i)); });
 #else
                     const RecRegs rr = load_rec(rec);
