@@ -226,6 +226,23 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
         zi = rint(mu + rs.u((uint32_t)(a.d - 1 - i)) * 1e-300);
     } else
 #endif
+#if defined(LGS_DISP_CODE) && defined(LGS_DISP_FIRST)
+    // the capped sigma >= 360 kind tested first, on the host's dispatch code (scalar),
+    // ahead of the sigma == 0 test (a vector compare and an exec-masked branch)
+    if (!LIBM && __builtin_amdgcn_readfirstlane((int)(__double_as_longlong(rr[kRecDisp]) >> 32)) == 0x3ff00000) {
+        const double u = rs.u((uint32_t)(a.d - 1 - i));
+        SzPair r;
+        r.ln = 0.0;
+        r.z = sample_z_capped<CERT>(mu, u, qh, RecView{rr}, WL, r.ln, dmu);
+        double ln = 0.0;
+        zi = sz_finish<CERT>(r, mu, u, rec, a.precision, a.linear_probs != 0, WL, etab, ln, dmu, amb);
+        if (WL) {
+            lw += ln;
+            tb += fabs(ln);
+            eb += amb ? 0.0 : wl_bound_generic(ln, qh.v[1], wl_window_hw(qh.v[6]), dmu);
+        }
+    } else
+#endif
     // CERT: a decision not covered by the certificate is returned as a guess with
     // amb set and no weight term (the sub-panel's verification adds it); selects
     // instead of early returns keep the weight update branch-free (measured 13 vs
@@ -1460,7 +1477,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                 cert_lds[1][threadIdx.x] = cert_lds[0][threadIdx.x];  // sum |z_j| before the sub-panel
                 cert_lds[2][threadIdx.x] = lw;
                 double z1e = cert_lds[0][threadIdx.x];
+                #ifdef LGS_HIST_STORE16  // (variant) every history value stored per coordinate: no register packing
+                const bool hblock = false;
+#else
                 const bool hblock = OZ && rows16 == 16;
+#endif
                 unsigned int hp[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) hp[j] = 0u;
@@ -1471,6 +1492,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                                   __builtin_amdgcn_readfirstlane((int)((lds_cdptr)rec_lds)[(top - 1 - (p_hi - 32)) * kRecStride + kRecSpec]) == 2;
 #endif
                 bool snz = false;  // (OZ) a nonzero z in this sub-panel, this lane
+#ifdef LGS_TAIL2
+                double zmx = 0.0, zmn = 0.0;  // the sub-panel's largest / smallest z (range checks, snz)
+                ZT* zrow = Z + (size_t)(top - 1) * ldz;  // row of the step's coordinate (uniform)
+                const uint32_t zoff = (uint32_t)p * (uint32_t)sizeof(ZT);  // this lane's byte offset in a row
+#endif
                 double zsq = 0.0;  // (q-panel skip) sum z^2 of this sub-panel, this lane
 #ifndef LGS_NEAR_UNROLL  // coordinates per loop iteration (the running sums shift by one per step)
 #define LGS_NEAR_UNROLL 1
@@ -1523,6 +1549,17 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     // stores: v_cvt_i32_f64 saturates, so no clamps -- a value beyond the
                     // int16 history's range (or a 16-bit store's) flags kFlagOverflow16 and
                     // the launch is redone wider; beyond int32 is an error (kFlagOverflow)
+#ifdef LGS_TAIL2
+                    // (the range checks from the sub-panel's extremes after the loop; the store
+                    // through the row's uniform base and a 32-bit lane offset)
+                    zmx = fmax(zmx, zi);
+                    zmn = fmin(zmn, zi);
+                    if constexpr (sizeof(ZT) == 8)
+                        *(ZT*)((char*)zrow + zoff) = (ZT)(int64_t)zi;
+                    else
+                        *(ZT*)((char*)zrow + zoff) = (ZT)(int)zi;
+                    zrow -= ldz;
+#else
                     if constexpr (sizeof(ZT) == 8) {
                         Z[(size_t)i * ldz + p] = (ZT)(int64_t)zi;
                     } else {
@@ -1530,8 +1567,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         if (!OZ && sizeof(ZT) == 2 && !(zi <= 32767.0 && zi >= -32768.0)) flags |= kFlagOverflow16;
                         Z[(size_t)i * ldz + p] = (ZT)(int)zi;
                     }
+#endif
                     if constexpr (OZ) {
+#ifndef LGS_TAIL2
                         if (!(zi <= 32639.0 && zi >= -32767.0)) flags |= kFlagOverflow16;
+#endif
                         // int16 history value z + 128 (exact whenever the range check passed)
                         const unsigned int hv = (unsigned int)((int)zi + 128) & 0xffffu;
                         if (hblock) {
@@ -1543,7 +1583,9 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                             a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] = (int16_t)hv;
                             if constexpr (!WL) zsq = fma(zi, zi, zsq);  // (whole sub-panels: from hp below)
                         }
+#ifndef LGS_TAIL2
                         snz |= zi != 0.0;
+#endif
                     }
                     // sum |z|: only the sub-panel's end reads it (the certificate's per-coordinate
                     // bound uses the cap), so a whole 16-row sub-panel takes it from the packed
@@ -1565,6 +1607,12 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     }
 #endif
                 }
+#ifdef LGS_TAIL2
+                if (sizeof(ZT) == 4 && !(zmx <= 2147483647.0 && zmn >= -2147483648.0)) flags |= kFlagOverflow;
+                if (!OZ && sizeof(ZT) == 2 && !(zmx <= 32767.0 && zmn >= -32768.0)) flags |= kFlagOverflow16;
+                if (OZ && !(zmx <= 32639.0 && zmn >= -32767.0)) flags |= kFlagOverflow16;
+                if constexpr (OZ) snz = zmx != 0.0 || zmn != 0.0;
+#endif
                 if constexpr (OZ) {
                     if (hblock) {
                         v4u_t* hp4 = (v4u_t*)(a.h16 + ((size_t)((top - 16 + a.h16_shift) >> 4) * a.h16_lanes + p) * 16);
