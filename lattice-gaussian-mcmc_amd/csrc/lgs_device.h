@@ -14,6 +14,29 @@
 
 #include "lgs_kernels.h"
 
+// Round-5 near-field trims of klein_mfma_kernel, on by default (LGS_R5_OFF: the
+// round-4 forms, for A/B): the range checks and the sub-panel's nonzero flag from its
+// extremes and Z stored through the row's uniform base (LGS_TAIL2), the SampleZ
+// dispatch from the host's code in the record (LGS_DISP_CODE), the capped quantile
+// test without short-circuit branches (LGS_CAP_BRANCHLESS), each coordinate's int16
+// history value stored at once instead of packed through 8 registers
+// (LGS_HIST_STORE16).  Together 2.47 -> 2.34-2.36 ms per 2^18 C3 samples, identical
+// outputs (profiles/r05f_kb_trims.log).
+#ifndef LGS_R5_OFF
+#ifndef LGS_TAIL2
+#define LGS_TAIL2 1
+#endif
+#ifndef LGS_DISP_CODE
+#define LGS_DISP_CODE 1
+#endif
+#ifndef LGS_CAP_BRANCHLESS
+#define LGS_CAP_BRANCHLESS 1
+#endif
+#ifndef LGS_HIST_STORE16
+#define LGS_HIST_STORE16 1
+#endif
+#endif
+
 namespace lgs {
 
 // Basis constants are never written by a kernel: reading them through the
@@ -98,12 +121,19 @@ struct CoordStreamT {
 #ifdef LGS_PHILOX2
     U4 w2;  // the quad's second pair
 #endif
+#ifdef LGS_PHILOX_NEXT
+    U4 wn;          // the next pair's block, drawn at the current pair's second slot
+    uint32_t pn;    // its pair index (0xffffffff = none)
+#endif
     __device__ __forceinline__ void init(uint64_t seed, uint32_t step_, uint32_t chain_) {
         k0 = (uint32_t)seed;
         k1 = (uint32_t)(seed >> 32);
         step = step_;
         chain = chain_;
         pair = 0xffffffffu;
+#ifdef LGS_PHILOX_NEXT
+        pn = 0xffffffffu;
+#endif
     }
     __device__ __forceinline__ double u(uint32_t slot) {
 #ifdef LGS_DIAG_CHEAP_RNG  // diagnostic builds only: Philox cost probe (wrong stream)
@@ -126,6 +156,28 @@ struct CoordStreamT {
             }
             const U4 ww = (slot & 2u) ? w2 : w;
             return (slot & 1u) ? u53(ww.z, ww.w) : u53(ww.x, ww.y);
+        }
+#endif
+#ifdef LGS_PHILOX_NEXT
+        // software-pipelined (the Klein kernels' wave-uniform slots, ascending): the block
+        // of pair p + 1 is drawn at pair p's second slot, a step before its first use,
+        // off that step's decision chain; a slot sequence that jumps (skipped
+        // sub-panels) draws its block in place
+        if constexpr (OPAQUE) {
+            const uint32_t p = __builtin_amdgcn_readfirstlane(slot >> 1);
+            if (p != __builtin_amdgcn_readfirstlane(pair)) {
+                if (p == __builtin_amdgcn_readfirstlane(pn))
+                    w = wn;
+                else
+                    w = philox4x32_10<true>(p, step, chain, kTagCoord, k0, k1);
+                pair = p;
+            }
+            const double r = (slot & 1u) ? u53(w.z, w.w) : u53(w.x, w.y);
+            if (slot & 1u) {
+                wn = philox4x32_10<true>(p + 1, step, chain, kTagCoord, k0, k1);
+                pn = p + 1;
+            }
+            return r;
         }
 #endif
         const uint32_t p = slot >> 1;

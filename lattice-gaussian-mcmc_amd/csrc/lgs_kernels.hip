@@ -1477,7 +1477,10 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                 cert_lds[1][threadIdx.x] = cert_lds[0][threadIdx.x];  // sum |z_j| before the sub-panel
                 cert_lds[2][threadIdx.x] = lw;
                 double z1e = cert_lds[0][threadIdx.x];
-                #ifdef LGS_HIST_STORE16  // (variant) every history value stored per coordinate: no register packing
+#ifdef LGS_HIST_STORE16
+                // (default) every coordinate's history value stored at once: the packing of a
+                // whole sub-panel through 8 registers (8 VALU per coordinate) cost more than
+                // the 16-bit store it saves (profiles/r05f_kb_trims.log)
                 const bool hblock = false;
 #else
                 const bool hblock = OZ && rows16 == 16;

@@ -9,7 +9,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-r02}
 CFG=${2:-C3_ntru512}
-ARGS="--steps 3 --warmup 1 --no-cpu --config $CFG"
+ARGS="--steps 3 --warmup 1 --no-cpu --wl-steps 0 --config $CFG"
 O=gpurun_out/prof_$TAG
 mkdir -p $O profiles
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py $ARGS > $O/bench_trace.log 2>&1 || { tail -20 $O/bench_trace.log; exit 1; }
