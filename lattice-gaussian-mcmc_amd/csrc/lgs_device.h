@@ -20,8 +20,9 @@
 // dispatch from the host's code in the record (LGS_DISP_CODE), the capped quantile
 // test without short-circuit branches (LGS_CAP_BRANCHLESS), each coordinate's int16
 // history value stored at once instead of packed through 8 registers
-// (LGS_HIST_STORE16).  Together 2.47 -> 2.34-2.36 ms per 2^18 C3 samples, identical
-// outputs (profiles/r05f_kb_trims.log).
+// (LGS_HIST_STORE16), and the tail's integer extremes / running history pointer
+// (LGS_TAIL3).  Together 2.47 -> 2.32-2.37 ms per 2^18 C3 samples, identical outputs
+// (profiles/r05f_kb_trims.log, r05h_kb.log).
 #ifndef LGS_R5_OFF
 #ifndef LGS_TAIL2
 #define LGS_TAIL2 1
@@ -34,6 +35,9 @@
 #endif
 #ifndef LGS_HIST_STORE16
 #define LGS_HIST_STORE16 1
+#endif
+#ifndef LGS_TAIL3  // (integer extremes, running history pointer, the uncovered mask behind a ballot)
+#define LGS_TAIL3 1
 #endif
 #endif
 

@@ -229,7 +229,7 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
 #if defined(LGS_DISP_CODE) && defined(LGS_DISP_FIRST)
     // the capped sigma >= 360 kind tested first, on the host's dispatch code (scalar),
     // ahead of the sigma == 0 test (a vector compare and an exec-masked branch)
-    if (!LIBM && __builtin_amdgcn_readfirstlane((int)(__double_as_longlong(rr[kRecDisp]) >> 32)) == 0x3ff00000) {
+    if (!LIBM && __builtin_amdgcn_readfirstlane(__double2hiint(rr[kRecDisp])) == 0x3ff00000) {
         const double u = rs.u((uint32_t)(a.d - 1 - i));
         SzPair r;
         r.ln = 0.0;
@@ -274,7 +274,7 @@ __device__ __forceinline__ double decide_coord_rec(const KleinArgs& a, int i, do
 #ifdef LGS_DISP_CODE
         // the host's dispatch code (kRecDisp): one scalar read of its high word (0 for
         // 0.0, 0x3ff00000 for 1.0) instead of converting the kind and testing q[7]
-        const int dsp = __builtin_amdgcn_readfirstlane((int)(__double_as_longlong(rr[kRecDisp]) >> 32));
+        const int dsp = __builtin_amdgcn_readfirstlane(__double2hiint(rr[kRecDisp]));
         const bool small_fast = dsp == 0, capped1 = dsp == 0x3ff00000;
 #else
         const int kind = __builtin_amdgcn_readfirstlane((int)qh.v[2]);
@@ -1495,6 +1495,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                                   __builtin_amdgcn_readfirstlane((int)((lds_cdptr)rec_lds)[(top - 1 - (p_hi - 32)) * kRecStride + kRecSpec]) == 2;
 #endif
                 bool snz = false;  // (OZ) a nonzero z in this sub-panel, this lane
+#ifdef LGS_TAIL3
+                int izmx = 0, izmn = 0;  // (16-bit stores) the same extremes of the saturated int32 values
+                int16_t* hptr = a.h16 + ((size_t)((top - 1 + a.h16_shift) >> 4) * a.h16_lanes + p) * 16 +
+                                ((top - 1 + a.h16_shift) & 15);
+#endif
 #ifdef LGS_TAIL2
                 double zmx = 0.0, zmn = 0.0;  // the sub-panel's largest / smallest z (range checks, snz)
                 ZT* zrow = Z + (size_t)(top - 1) * ldz;  // row of the step's coordinate (uniform)
@@ -1537,7 +1542,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                         a, i, mu, rec, rr, rs, lw, flags, etab_s,
                         cert_dmu(rr[kSzCa], coarse ? rec[kRecCbC] : rr[kSzCb], a.z1cap, mu), un, eb, tb);
 #endif
+#ifdef LGS_TAIL3
+                    if (__builtin_amdgcn_ballot_w64(un) != 0) flm |= un ? (1 << s) : 0;  // (rare)
+#else
                     flm |= un ? (1 << s) : 0;
+#endif
 #if defined(LGS_DIAG_CYCLES) && !defined(LGS_DIAG_STEP)
                     {
                         LGS_DC_T(t_sz1);
@@ -1555,12 +1564,27 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
 #ifdef LGS_TAIL2
                     // (the range checks from the sub-panel's extremes after the loop; the store
                     // through the row's uniform base and a 32-bit lane offset)
+#ifdef LGS_TAIL3
+                    // 16-bit stores: the extremes of the saturated int32 conversion (one
+                    // v_max_i32 / v_min_i32; fmax would canonicalise both operands first)
+                    // detect every value outside the int16 / history range as well
+                    const int zint = (int)zi;
+                    if constexpr (sizeof(ZT) <= 2) {
+                        izmx = max(izmx, zint);
+                        izmn = min(izmn, zint);
+                    } else {
+                        zmx = fmax(zmx, zi);
+                        zmn = fmin(zmn, zi);
+                    }
+#else
+                    const int zint = (int)zi;
                     zmx = fmax(zmx, zi);
                     zmn = fmin(zmn, zi);
+#endif
                     if constexpr (sizeof(ZT) == 8)
                         *(ZT*)((char*)zrow + zoff) = (ZT)(int64_t)zi;
                     else
-                        *(ZT*)((char*)zrow + zoff) = (ZT)(int)zi;
+                        *(ZT*)((char*)zrow + zoff) = (ZT)zint;
                     zrow -= ldz;
 #else
                     if constexpr (sizeof(ZT) == 8) {
@@ -1582,8 +1606,15 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                             for (int j = 7; j >= 1; --j) hp[j] = __builtin_amdgcn_alignbit(hp[j], hp[j - 1], 16);
                             hp[0] = (hp[0] << 16) | hv;
                         } else {
+#ifdef LGS_TAIL3
+                            // a sub-panel lies in one 16-coordinate history block ((top + shift)
+                            // % 16 == 0): step s writes position 15 - s of this lane's block
+                            *hptr = (int16_t)hv;
+                            --hptr;
+#else
                             const int ih = i + a.h16_shift;
                             a.h16[((size_t)(ih >> 4) * a.h16_lanes + p) * 16 + (ih & 15)] = (int16_t)hv;
+#endif
                             if constexpr (!WL) zsq = fma(zi, zi, zsq);  // (whole sub-panels: from hp below)
                         }
 #ifndef LGS_TAIL2
@@ -1610,6 +1641,12 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     }
 #endif
                 }
+#ifdef LGS_TAIL3
+                if constexpr (sizeof(ZT) <= 2) {
+                    zmx = (double)izmx;
+                    zmn = (double)izmn;
+                }
+#endif
 #ifdef LGS_TAIL2
                 if (sizeof(ZT) == 4 && !(zmx <= 2147483647.0 && zmn >= -2147483648.0)) flags |= kFlagOverflow;
                 if (!OZ && sizeof(ZT) == 2 && !(zmx <= 32767.0 && zmn >= -32768.0)) flags |= kFlagOverflow16;
