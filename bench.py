@@ -473,7 +473,12 @@ def main():
         "roofline": roofline,
         "gemm": gemm,
         "kernel_ms": {"klein": round(k_ms / max(k_n, 1), 3), "bz": round(g_ms / max(g_n, 1), 3),
-                      "accept": round(a_ms / max(a_n, 1), 3), "moments": round(m_ms / max(m_n, 1), 3)},
+                      "accept": round(a_ms / max(a_n, 1), 3), "moments": round(m_ms / max(m_n, 1), 3),
+                      "blocks_pipelined": os.environ.get("LGS_NO_PIPE") != "1",
+                      "note": "pipelined blocks: each lgs_imhk block's Klein launch runs on the library's Klein "
+                              "stream beside the previous block's accept / moments / B z on the work stream, so "
+                              "these launch times overlap (their sum exceeds ms_per_step) and each is stretched by "
+                              "sharing the CUs; LGS_NO_PIPE=1 gives isolated launches"},
         "cpu_baseline": cpu,
         "wang_ling": wang_ling,
         "device": dinfo["name"],

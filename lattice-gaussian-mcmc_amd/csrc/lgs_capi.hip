@@ -162,6 +162,20 @@ struct lgs_ctx {
     // abort producers, copied into pinned host memory, and the event after that copy
     unsigned int* fw_host = nullptr;
     hipEvent_t fw_ev = nullptr;
+    // Pipelined blocks (lgs_imhk with the early check): each block's Klein launch runs
+    // on kstream into one of two buffer sets (proposal store, weights, int16 history,
+    // zero flags, flag words), so the next block's -- or the next call's -- launch
+    // runs beside this block's accept / moments / B z on the caller's stream (IMHK
+    // proposals do not depend on the chain state).  ev_free: recorded on the caller's
+    // stream after the set's last reader; the set's next Klein launch waits for it.
+    struct BlockSet {
+        DevBuf Z, LW, H16, ZNZ, CLIVE, flags;
+        hipEvent_t ev_free = nullptr;
+        bool free_recorded = false;
+    } bset[2];
+    int bset_next = 0;
+    hipStream_t kstream = nullptr;
+    hipEvent_t ev_klein = nullptr;
 };
 
 namespace {
@@ -206,6 +220,40 @@ struct Scope {  // times one launch when timing is enabled
 };
 
 int run_bz_fp64(lgs_ctx* c, const BzCall& b);
+
+void swap_buf(DevBuf& a, DevBuf& b) {
+    std::swap(a.p, b.p);
+    std::swap(a.bytes, b.bytes);
+}
+
+// A pipelined block's buffer set swapped into the context's working buffers (which
+// every launch path uses), and back on every exit from the block.  The flag words
+// first: the block's initial draws (into the context's own store) already report
+// into them; then the store, for the block's own Klein launch and its dependants.
+struct SetSwap {
+    lgs_ctx* c = nullptr;
+    int j = -1;
+    bool flags_in = false, store_in = false;
+    void swap_flags() {
+        swap_buf(c->flags, c->bset[j].flags);
+        flags_in = !flags_in;
+    }
+    void swap_store() {
+        auto& s = c->bset[j];
+        swap_buf(c->Z, s.Z);
+        swap_buf(c->LW, s.LW);
+        swap_buf(c->H16, s.H16);
+        swap_buf(c->ZNZ, s.ZNZ);
+        swap_buf(c->CLIVE, s.CLIVE);
+        store_in = !store_in;
+    }
+    void restore() {
+        if (j < 0) return;
+        if (store_in) swap_store();
+        if (flags_in) swap_flags();
+    }
+    ~SetSwap() { restore(); }
+};
 
 // Wait for the stream; if an int8-digit B z saw a coefficient beyond two digits,
 // replay the pending B z launches with the fp64 kernel.  Must run before any
@@ -525,6 +573,11 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
     Scope s(c, 1);
     const int8_t* hi = c->Bd.as<int8_t>();
     const int8_t* lo = hi + (size_t)c->bd_rows * c->bd_cols;
+    // timing probes only (wrong outputs): LGS_DIAG_BZ=1 drops the ||v||^2 rows, 2 the
+    // selections (row q reads proposal q), 3 both
+    static const int diag_bz = getenv("LGS_DIAG_BZ") ? atoi(getenv("LGS_DIAG_BZ")) : 0;
+    if (diag_bz & 1) VN = nullptr;
+    if (diag_bz & 2) sel = nullptr;
     double* VNP = nullptr;
     if (VN) {
         const int rc = c->VNP.reserve((size_t)2 * ((c->d + 127) / 128) * vn_n * 8);
@@ -659,6 +712,13 @@ int lgs_destroy(lgs_ctx* c) {
     for (auto e : c->pool) (void)hipEventDestroy(e);
     if (c->fw_ev) (void)hipEventDestroy(c->fw_ev);
     if (c->fw_host) (void)hipHostFree(c->fw_host);
+    if (c->kstream) {
+        (void)hipStreamSynchronize(c->kstream);
+        (void)hipStreamDestroy(c->kstream);
+    }
+    if (c->ev_klein) (void)hipEventDestroy(c->ev_klein);
+    for (auto& s : c->bset)
+        if (s.ev_free) (void)hipEventDestroy(s.ev_free);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
     return LGS_OK;
@@ -671,6 +731,7 @@ int lgs_set_stream(lgs_ctx* c, void* s) {
     // the old stream may still run an early-checked lgs_imhk's later launches, which
     // read the context's buffers: finish them before another stream reuses those
     if (ns != c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->kstream) HIP_TRY(hipStreamSynchronize(c->kstream));
     c->stream = ns;
     return LGS_OK;
 }
@@ -1271,8 +1332,39 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
     // proposal store: np columns, plus nc columns for the chain states carried into a
     // block when lattice points are requested (kept-state selections become plain columns)
     const bool carry = v_samples != nullptr;
-    if ((rc = c->Z.reserve((size_t)(np + (carry ? nc : 0)) * d * std::max(zb, 4))) ||
-        (rc = c->LW.reserve((size_t)np * 8)) ||
+    // pipelined blocks (see lgs_ctx::BlockSet): the context's own store then only takes
+    // the initial draws (nc columns); LGS_NO_PIPE=1: A/B
+    static const bool no_pipe = getenv("LGS_NO_PIPE") && atoi(getenv("LGS_NO_PIPE")) == 1;
+    const bool pipe = early && !no_pipe && n_steps > 0;
+    const int64_t own_cols = pipe ? nc : np + (carry ? nc : 0);
+    if (pipe) {
+        if (!c->kstream) {
+            // LGS_PIPE_PRIO=1: at the device's highest priority, so the Klein launch's
+            // workgroups are dispatched first (measured: no gain, 102.3-102.4 vs
+            // 102.6-102.9 M samples/s at the default priority, profiles/r05k_*)
+            static const bool prio = getenv("LGS_PIPE_PRIO") && atoi(getenv("LGS_PIPE_PRIO")) == 1;
+            int plo = 0, phi = 0;
+            if (prio && hipDeviceGetStreamPriorityRange(&plo, &phi) == hipSuccess && phi != plo)
+                HIP_TRY(hipStreamCreateWithPriority(&c->kstream, hipStreamNonBlocking, phi));
+            else
+                HIP_TRY(hipStreamCreateWithFlags(&c->kstream, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&c->ev_klein, hipEventDisableTiming));
+        }
+        for (auto& s : c->bset) {
+            if (!s.ev_free) HIP_TRY(hipEventCreateWithFlags(&s.ev_free, hipEventDisableTiming));
+            if (!s.flags.p) {
+                if ((rc = s.flags.reserve(4 * lgs::kFlagWords))) return rc;
+                HIP_TRY(hipMemset(s.flags.p, 0, 4 * lgs::kFlagWords));
+            }
+            // (a set in use by an earlier call's dependants is never grown here: the
+            // sizes depend on nc, T and d only, and hipFree waits for the device)
+            if ((rc = s.Z.reserve((size_t)(np + (carry ? nc : 0)) * d * std::max(zb, 4))) ||
+                (rc = s.LW.reserve((size_t)np * 8)))
+                return rc;
+        }
+    }
+    if ((rc = c->Z.reserve((size_t)own_cols * d * std::max(zb, 4))) ||
+        (rc = c->LW.reserve((size_t)(pipe ? nc : np) * 8)) ||
         (rc = c->sel.reserve((size_t)std::max<int64_t>(nc * kmax, nc) * 8)) ||
         (rc = c->fsel.reserve((size_t)nc * 8)) || (rc = c->cnt.reserve((size_t)np * 4)) ||
         (rc = c->ccnt.reserve((size_t)nc * 4)) || (certw && (rc = c->LWE.reserve((size_t)np * 8))))
@@ -1324,6 +1416,13 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
     // skipped on the device (kAbortMask) and is redone at the wider width.
     for (int64_t t0 = 0; t0 < n_steps || t0 == 0;) {
         bool oz_used = false;
+        SetSwap sw;  // (pipe) this block's buffer set, swapped back on every exit
+        if (pipe) {
+            sw.c = c;
+            sw.j = c->bset_next;
+            sw.swap_flags();
+            fl = c->flags.as<unsigned int>();
+        }
         // ---- initial draws (counter step 0) of uninitialised chains (imhk.py:126-139),
         // decided on the device: the Klein launch and its application are gated by
         // "some chain has init == 0" (block 0 of the call only)
@@ -1355,6 +1454,7 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
         const int64_t npb = nc * Tb;
         const int64_t first_keep = t0 / thin;  // t0 is a multiple of thin
         const int64_t kb = std::min<int64_t>(Tb / thin, n_keep - first_keep);
+        if (pipe) sw.swap_store();  // the block's store, weights and history from here on
         lgs::KleinArgs a = base_args(c, seed);
         a.counter_mode = 1;
         a.chain0 = (uint32_t)first_chain;
@@ -1369,7 +1469,19 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             a.emax = c->EMAX.as<unsigned long long>();
         }
         bool ozb = false;
-        if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p, true, &ozb))) return rc;
+        if (pipe) {  // on kstream, once the set's last reader (two blocks back) is done
+            auto& bs = c->bset[sw.j];
+            if (bs.free_recorded) HIP_TRY(hipStreamWaitEvent(c->kstream, bs.ev_free, 0));
+            const hipStream_t cs = c->stream;
+            c->stream = c->kstream;
+            rc = run_klein_store(c, a, exact, wl, zb, c->Z.p, true, &ozb);
+            c->stream = cs;
+            if (rc) return rc;
+            HIP_TRY(hipEventRecord(c->ev_klein, c->kstream));
+            HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_klein, 0));
+        } else if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p, true, &ozb))) {
+            return rc;
+        }
         oz_used |= ozb;
         // chain states carried into the block's store (a state beyond 16 bits flags kFlagCarry16)
         if (carry && kb > 0)
@@ -1486,6 +1598,15 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
                                           (int)d, zs, cm, c->stream, fl));
         bool redo = false;
         if ((rc = finish_or_redo(c, oz_used, zb, redo, early))) return rc;
+        if (pipe) {  // the set's readers are all enqueued (its flag words reset behind them)
+            const int j = sw.j;
+            sw.restore();
+            sw.j = -1;
+            fl = c->flags.as<unsigned int>();
+            HIP_TRY(hipEventRecord(c->bset[j].ev_free, c->stream));
+            c->bset[j].free_recorded = true;
+            if (!redo) c->bset_next ^= 1;
+        }
         if (redo) continue;  // same block again (block 0: its initial draws too)
         t0 += T;
     }

@@ -2654,18 +2654,53 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
     const bool use_clive = KPT == 16 && h16 != nullptr && clive != nullptr;
     const bool use_znz = !use_clive && KPT == 16 && h16 != nullptr && znz != nullptr;
     __shared__ unsigned int livew[kOzMaxD / 64 / 32];
+    // (round 5) every wave ORs the words itself: the 4 waves hold the same 64 samples
+    // (zm = lane), so no LDS round trip and barrier precede the first chunk's loads;
+    // the word stays in a scalar register up to d = 2048, else in the wave's LDS row
+    __shared__ unsigned int livew4[4][kOzMaxD / 64 / 32];
+    const int ngw = (d + 2047) / 2048;
+    unsigned int live1 = 0u;
     if (use_clive) {
-        if (wave == 0) {  // threads tid < 64: zq = 0, one sample per lane
-            const int ng = (d + 2047) / 2048;
+        {
+            const int ng = ngw;
+#ifndef LGS_BZ_NO_GUESS
+            // the word of the identity selection (row q = proposal q: every kept state a
+            // fresh proposal, e.g. acceptance 1) is loaded beside the selection itself
+            // instead of after it; a lane whose selection differs reloads
+            const int64_t zg = zs_ < n ? zs_ : 0;
+            const unsigned int wg0 = zg < hcols ? clive[zg >> 6] : 0xffffffffu;
+            const bool same = (zcol >> 6) == (zg >> 6) && (zcol < hcols) == (zg < hcols);
+#endif
             for (int g = 0; g < ng; ++g) {
                 unsigned int w = 0u;
+#ifndef LGS_BZ_NO_GUESS
+                const unsigned int wg =
+                    g == 0 ? wg0 : (zg < hcols ? clive[(size_t)g * clive_ld + (zg >> 6)] : 0xffffffffu);
+                if (zs_ < n)
+                    w = same ? wg : (zcol < hcols ? clive[(size_t)g * clive_ld + (zcol >> 6)] : 0xffffffffu);
+#else
                 if (zs_ < n) w = zcol < hcols ? clive[(size_t)g * clive_ld + (zcol >> 6)] : 0xffffffffu;
+#endif
+                // OR over the wave's lanes; all equal (the tile's samples from one Klein
+                // wave) needs no shuffles
+                const unsigned int w0 = __builtin_amdgcn_readfirstlane(w);
+                if (__builtin_amdgcn_ballot_w64(w != w0) != 0ull) {
 #pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) w |= __shfl_xor(w, o);
-                if (lane == 0) livew[g] = w;
+                    for (int o = 32; o >= 1; o >>= 1) w |= __shfl_xor(w, o);
+                } else {
+                    w = w0;
+                }
+                if (ng == 1)
+                    live1 = __builtin_amdgcn_readfirstlane(w);
+                else if (lane == 0)
+                    livew4[wave][g] = w;
+            }
+            if (ng > 1) {  // the wave's own LDS row: in order within the wave
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
         }
-        __syncthreads();
     }
     if (use_znz) {
         const bool hp = zs_ < n && zcol < hcols;
@@ -2680,7 +2715,7 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
     }
     for (int ci = ci0; ci < ci1; ++ci) {
         const int cix = kchunk[ci];
-        if (use_clive && !((livew[cix >> 5] >> (cix & 31)) & 1u)) continue;  // (uniform)
+        if (use_clive && !(((ngw == 1 ? live1 : livew4[wave][cix >> 5]) >> (cix & 31)) & 1u)) continue;  // (uniform)
         if (use_znz && !((livew[(ci - ci0) >> 5] >> ((ci - ci0) & 31)) & 1u)) continue;  // (uniform)
         const int c0 = cix * KC;
         if (KPT == 16 && h16 != nullptr && zs_ < n && zcol < hcols) {

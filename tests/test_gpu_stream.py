@@ -365,3 +365,85 @@ def test_early_check_equals_synchronised_call(capi, zmax):
             assert np.array_equal(got, w)
         else:
             np.testing.assert_allclose(got, w, rtol=1e-12, atol=0)
+
+
+def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, blocks: int = 3):
+    """Several lgs_imhk_ex calls of several blocks each (LGS_MAX_PROPOSALS: T = 4 steps
+    per block), chain state, accept counts, moments, lattice points, functionals and
+    lag sums carried across them -- on a caller's stream the blocks are pipelined
+    (each block's Klein launch on the context's Klein stream into alternating buffer
+    sets, beside the previous block's dependants)."""
+    import torch
+    from conftest import golden_R, load_golden
+    g = load_golden("klein_qary128.npz")
+    R, cp, B = golden_R(g)
+    d, nc, T = R.shape[0], 256, 4
+    old = os.environ.get("LGS_MAX_PROPOSALS")
+    os.environ["LGS_MAX_PROPOSALS"] = str(nc * T)
+    try:
+        ctx = capi.Context(0)
+    finally:
+        if old is None:
+            del os.environ["LGS_MAX_PROPOSALS"]
+        else:
+            os.environ["LGS_MAX_PROPOSALS"] = old
+    ctx.set_basis(R, cp, B, float(g["sigma"]))
+    dev = "cuda:0"
+    steps = T * blocks
+    z = torch.zeros((d, nc), dtype=torch.int32, device=dev)
+    lw = torch.zeros(nc, dtype=torch.float64, device=dev)
+    init = torch.zeros(nc, dtype=torch.int32, device=dev)
+    acc = torch.zeros(nc, dtype=torch.int64, device=dev)
+    mom = torch.zeros(2 * d, dtype=torch.int64, device=dev)
+    L = 5
+    zr = torch.zeros((nc, L), dtype=torch.int64, device=dev)
+    zsum = torch.zeros(L + 2, dtype=torch.int64, device=dev)
+    vr = torch.zeros((nc, L), dtype=torch.float64, device=dev)
+    vsum = torch.zeros(L + 2, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream(device=dev)
+    if on_caller_stream:
+        ctx.set_stream(s.cuda_stream)
+    vs_all, vn_all, zk_all = [], [], []
+    with torch.cuda.stream(s):
+        for call in range(calls):
+            vs = torch.zeros((nc, steps, d), dtype=torch.float64, device=dev)
+            vn2 = torch.zeros((nc, steps), dtype=torch.float64, device=dev)
+            zk = torch.zeros((nc, steps), dtype=torch.int64, device=dev)
+            ctx.imhk(11, 0, nc, 1 + call * steps, steps, 1, z, lw, init, acc, v_samples=vs, moments=mom,
+                     vnorm2_samples=vn2, zk_samples=zk, zk_index=5,
+                     flags=capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR | flags_extra,
+                     lag=(L, zr, zsum, vr, vsum, 1e-6))
+            vs_all.append(vs)
+            vn_all.append(vn2)
+            zk_all.append(zk)
+    torch.cuda.synchronize()
+    out = {k: t.cpu().numpy() for k, t in dict(z=z, lw=lw, init=init, acc=acc, mom=mom, zsum=zsum, vsum=vsum,
+                                                 zr=zr, vr=vr).items()}
+    out["v"] = torch.cat(vs_all, 1).cpu().numpy()
+    out["vn2"] = torch.cat(vn_all, 1).cpu().numpy()
+    out["zk"] = torch.cat(zk_all, 1).cpu().numpy()
+    ctx.close()
+    return B, out
+
+
+@pytest.mark.parametrize("mode", ["reference", "wang_ling_exact"])
+def test_pipelined_blocks_equal_synchronised_calls(capi, mode):
+    """Pipelined blocks (caller's stream) give every output of the host-checked calls
+    on the library's own stream, bit for bit, over 3 calls x 3 blocks; v is B z of the
+    kept states (z_k recovered from v through the basis' inverse is checked against
+    zk)."""
+    fx = 0 if mode == "reference" else capi.LGS_WANG_LING | capi.LGS_EXACT_ORDER
+    B, a = _imhk_calls(capi, True, fx)
+    _, b = _imhk_calls(capi, False, fx)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    steps = a["v"].shape[1]
+    assert a["acc"].sum() > 0 and (mode == "reference") == bool((a["acc"] == steps).all())
+    # v = B z: z = B^-1 v is integral and its coordinate 5 is the zk series
+    zrec = np.rint(np.linalg.solve(B.astype(np.float64), a["v"].reshape(-1, B.shape[0]).T)).T
+    assert np.array_equal(zrec[:, 5].astype(np.int64), a["zk"].reshape(-1))
+    np.testing.assert_allclose(a["vn2"].reshape(-1), (a["v"].reshape(-1, B.shape[0]) ** 2).sum(1), rtol=1e-13)
+    # moments: sum over every kept state of z and z^2 (exact integers)
+    assert np.array_equal(a["mom"][:B.shape[0]], zrec.astype(np.int64).sum(0))
+    assert np.array_equal(a["mom"][B.shape[0]:], (zrec.astype(np.int64) ** 2).sum(0))
