@@ -132,6 +132,8 @@ struct lgs_ctx {
     } hist;
     DevBuf Bd;                    // int8 digit planes of B (hi | lo), [row][k], k padded to 64
     DevBuf kchunk, koff;          // per 128-row tile of B: the 64-column chunks with a non-zero digit
+    bool bz_mom_ok = false;       // every 64-column chunk has an owner tile (B z can sum the moments)
+    DevBuf MP;                    // B z's moment partials per (64-row tile, coordinate)
     DevBuf etab;                  // SampleZ erf/exp table (lgs_device.h erf_gauss)
     DevBuf etab2;                 // its Taylor-coefficient form (lgs_device.h CoefTab)
     DevBuf szc;                   // per-coordinate SampleZ constants (lgs_kernels.h kSzc*)
@@ -557,7 +559,8 @@ int run_bz_fp64(lgs_ctx* c, const BzCall& b) {
 int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
            int64_t rb = 0, int64_t rstride = 0, int64_t roff = 0, const int64_t* sel = nullptr,
            bool after_klein = false, const unsigned int* abort = nullptr, double* VN = nullptr,
-           int64_t vn_n = -1, bool device_replay = false) {
+           int64_t vn_n = -1, bool device_replay = false, unsigned long long* MP = nullptr,
+           int64_t mp_ld = 0, unsigned int* MPL = nullptr) {
     if (!c->has_B) return fail(LGS_ERR_STATE, "lattice points need B (lgs_set_basis B != NULL)");
     if (vn_n < 0 || vn_n > n) vn_n = n;  // ||v||^2 of the leading vn_n rows only
     if (vn_n == 0) VN = nullptr;
@@ -590,7 +593,7 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
                                after_klein && c->hist.Z == Z && Z ? c->H16.as<int16_t>() : nullptr, c->hist.lanes,
                                c->hist.cols, c->stream, abort, c->ZNZ.as<uint8_t>(),
                                after_klein && c->hist.Z == Z && Z ? c->hist.clive : nullptr, c->hist.clive_ld,
-                               VNP, vn_n));
+                               VNP, vn_n, MP, mp_ld, MPL));
     if (VN) HIP_TRY(lgs::launch::vnorm2_reduce(VNP, (int)c->d, vn_n, b.rb, b.rstride, b.roff, VN, c->stream, abort));
     if (device_replay) {  // the fp64 replay enqueued now, run only if the digit-range flag is set
         c->i8_dev_replay = true;
@@ -1043,18 +1046,26 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
             HIP_TRY(hipMemcpy(c->Bd.p, planes.data(), planes.size(), hipMemcpyHostToDevice));
             // block sparsity of B for bz_i8_kernel: an all-zero 128 x 64 block contributes
             // exactly nothing, so its K chunk is skipped (NTRU [[qI,0],[H,I]]: 62% of blocks)
+            // (bit 16 of an entry: the first row tile listing the chunk owns its share of
+            // the kept states' moments when B z computes them, bz_i8_kernel MP; B has full
+            // rank, so every chunk has an owner)
             std::vector<int> kc, ko(1, 0);
+            std::vector<char> owned((size_t)(cols / 64), 0);
             for (int64_t rt = 0; rt < rows / 128; ++rt) {
                 for (int64_t ch = 0; ch < cols / 64; ++ch) {
                     bool nz = false;
                     for (int64_t r = rt * 128; r < rt * 128 + 128 && !nz; ++r)
                         for (int64_t k = ch * 64; k < ch * 64 + 64 && !nz; ++k)
                             nz = hi[r * cols + k] != 0 || lo[r * cols + k] != 0;
-                    if (nz) kc.push_back((int)ch);
+                    if (nz) {
+                        kc.push_back((int)ch | (owned[ch] ? 0 : 1 << 16));
+                        owned[ch] = 1;
+                    }
                 }
                 ko.push_back((int)kc.size());
             }
             if (kc.empty()) kc.push_back(0);
+            c->bz_mom_ok = std::all_of(owned.begin(), owned.end(), [](char o) { return o != 0; });
             if ((rc = c->kchunk.reserve(kc.size() * 4)) || (rc = c->koff.reserve(ko.size() * 4))) return rc;
             HIP_TRY(hipMemcpy(c->kchunk.p, kc.data(), kc.size() * 4, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(c->koff.p, ko.data(), ko.size() * 4, hipMemcpyHostToDevice));
@@ -1341,11 +1352,12 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
         if (!c->kstream) {
             // LGS_PIPE_PRIO=1: at the device's highest priority, so the Klein launch's
             // workgroups are dispatched first (measured: no gain, 102.3-102.4 vs
-            // 102.6-102.9 M samples/s at the default priority, profiles/r05k_*)
-            static const bool prio = getenv("LGS_PIPE_PRIO") && atoi(getenv("LGS_PIPE_PRIO")) == 1;
+            // 102.6-102.9 M samples/s at the default priority, profiles/r05k_*);
+            // 2: at the lowest, so the previous block's dependants go first
+            static const int prio = getenv("LGS_PIPE_PRIO") ? atoi(getenv("LGS_PIPE_PRIO")) : 0;
             int plo = 0, phi = 0;
             if (prio && hipDeviceGetStreamPriorityRange(&plo, &phi) == hipSuccess && phi != plo)
-                HIP_TRY(hipStreamCreateWithPriority(&c->kstream, hipStreamNonBlocking, phi));
+                HIP_TRY(hipStreamCreateWithPriority(&c->kstream, hipStreamNonBlocking, prio == 1 ? phi : plo));
             else
                 HIP_TRY(hipStreamCreateWithFlags(&c->kstream, hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&c->ev_klein, hipEventDisableTiming));
@@ -1536,9 +1548,22 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
         }
         // The final-state gather rides on the moments pass unless a later step of this
         // block still reads the carried-in states (kept-state gather without carry columns).
-        const bool fuse_final = moments && !((z_samples || zk_samples) && kb > 0 && !carry) &&
+        // (round 5) the kept states' moments from B z's digit tiles: with every step kept
+        // (thin 1) the kept rows are exactly the states the moments count (proposals by
+        // their keep counts, carried states through their carry columns), and B z holds
+        // each row's digits in LDS anyway; the owning row tile sums each chunk's
+        // coordinates over its 64 rows (bz_i8_kernel MP) and a column reduction adds
+        // them up.  A carried |z| beyond two digits (B z's digit-range flag) falls back to
+        // the moments pass, gated on that flag on the device.  The chains' final states
+        // then come from the int16 history.  LGS_NO_BZ_MOMENTS=1: the separate pass.
+        static const bool no_bz_mom = getenv("LGS_NO_BZ_MOMENTS") && atoi(getenv("LGS_NO_BZ_MOMENTS")) == 1;
+        static const bool bz_f64 = getenv("LGS_BZ_FP64") && atoi(getenv("LGS_BZ_FP64")) == 1;
+        const bool bz_mom = moments && v_samples && early && thin == 1 && kb == Tb && kb > 0 && zb == 2 &&
+                            c->has_Bi8 && c->bz_mom_ok && !bz_f64 && c->hist.Z == c->Z.p && c->hist.Z &&
+                            d % 16 == 0 && d <= lgs::kOzMaxD && npb < ((int64_t)1 << 32) && !no_bz_mom;
+        const bool fuse_final = !bz_mom && moments && !((z_samples || zk_samples) && kb > 0 && !carry) &&
                                 npb < ((int64_t)1 << 32);
-        if (moments) {
+        if (moments && !bz_mom) {
             Scope s(c, 3);
             // carried-in states first: the fused pass overwrites z_state
             HIP_TRY(lgs::launch::moments_carry(zs, ob, cm, nc, (int)d, c->ccnt.as<int32_t>(), mom, c->stream, fl));
@@ -1561,9 +1586,28 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
                 // consumers, when the host cannot replay it first: the early check, and the
                 // lag sums below, which read ||v||^2 inside this call
                 const bool dev_replay = early || (lag && lag->lag_v_sums && vnorm2_samples);
+                const int64_t ntiles = (nq + 63) / 64, mp_ld = c->bd_cols;
+                const int64_t ngw = (d + 2047) / 2048;
+                unsigned int* mpl = nullptr;
+                if (bz_mom) {
+                    if ((rc = c->MP.reserve((size_t)ntiles * (mp_ld * 8 + ngw * 4)))) return rc;
+                    mpl = (unsigned int*)(c->MP.as<unsigned long long>() + (size_t)ntiles * mp_ld);
+                }
                 if ((rc = run_bz(c, c->Z.p, zb, ldzb, nq, v_samples, kb, n_keep, first_keep,
-                                 c->sel.as<int64_t>(), true, fl, vnorm2_samples, fn_chains * kb, dev_replay)))
+                                 c->sel.as<int64_t>(), true, fl, vnorm2_samples, fn_chains * kb, dev_replay,
+                                 bz_mom ? c->MP.as<unsigned long long>() : nullptr, mp_ld, mpl)))
                     return rc;
+                if (bz_mom) {
+                    Scope s(c, 3);
+                    HIP_TRY(lgs::launch::bz_moments_reduce(c->MP.as<unsigned long long>(), mpl, ntiles, mp_ld,
+                                                           (int)d, mom, fl, c->stream, fl));
+                    // (the fallback, run only when B z flagged a coefficient beyond its digits)
+                    HIP_TRY(lgs::launch::moments_carry(zs, ob, cm, nc, (int)d, c->ccnt.as<int32_t>(), mom,
+                                                       c->stream, fl, fl));
+                    HIP_TRY(lgs::launch::moments_final(c->Z.p, zb, ldzb, c->cnt.as<int32_t>(), npb, Tb, nullptr,
+                                                       (int)d, mom, zs, ob, cm, nc, c->stream, fl,
+                                                       c->ZNZ.as<uint8_t>(), c->hist.lanes, 0, fl));
+                }
             }
             if (zk_samples)  // (the leading fn_chains chains' kept states: q < fn_chains * kb)
                 HIP_TRY(lgs::launch::coord_gather(c->Z.p, zb, ldzb, c->sel.as<int64_t>(), fn_chains * kb, kb, zs, ob, cm, nc,
@@ -1593,7 +1637,10 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             }
         }
         // chain states after the block (in place; carried chains keep their row)
-        if (!fuse_final)
+        if (bz_mom)
+            HIP_TRY(lgs::launch::final_h16(c->H16.as<int16_t>(), c->hist.lanes, c->fsel.as<int64_t>(), nc, (int)d,
+                                           zs, ob, cm, c->stream, fl));
+        else if (!fuse_final)
             HIP_TRY(lgs::launch::gather_z(c->Z.p, zb, ldzb, c->fsel.as<int64_t>(), nc, 1, zs, ob, cm, nc,
                                           (int)d, zs, cm, c->stream, fl));
         bool redo = false;

@@ -275,10 +275,11 @@ hipError_t log_density(const KleinArgs& a, const double* R, const void* Z, int z
 hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int64_t T,
                          const int64_t* fsel, int d, unsigned long long* mom, void* zs, int ob,
                          int zs_cm, int64_t nc, hipStream_t st, const unsigned int* abort,
-                         const uint8_t* znz = nullptr, int64_t zlanes = 0, int zshift = 0);
+                         const uint8_t* znz = nullptr, int64_t zlanes = 0, int zshift = 0,
+                         const unsigned int* need = nullptr);
 hipError_t moments_carry(const void* zs, int zb, int coord_major, int64_t nc, int d,
                          const int32_t* cc, unsigned long long* mom, hipStream_t st,
-                         const unsigned int* abort = nullptr);
+                         const unsigned int* abort = nullptr, const unsigned int* need = nullptr);
 hipError_t gather_z(const void* Z, int zb, int64_t ldz, const int64_t* sel, int64_t nq,
                     int64_t q_per_chain, const void* zs, int ob, int zs_coord_major, int64_t nc,
                     int d, void* out, int out_coord_major, hipStream_t st,
@@ -304,7 +305,20 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
                  hipStream_t st, const unsigned int* abort = nullptr, const uint8_t* znz = nullptr,
                  const unsigned int* clive = nullptr, int64_t clive_ld = 0, double* VNP = nullptr,
-                 int64_t vn_n = 0);
+                 int64_t vn_n = 0, unsigned long long* MP = nullptr, int64_t mp_ld = 0,
+                 unsigned int* MPL = nullptr);
+// moments of the kept states from bz_i8's per-(tile, coordinate) partials MP (packed
+// sum over the tile's 64 rows of z^2 * 2^24 + z + 32768; MPL: the tile's live-chunk
+// words, (d + 2047) / 2048 per tile), added to mom (2d); returns at once when *flags has
+// kFlagI8Range (the gated moments pass replaces it then)
+hipError_t bz_moments_reduce(const unsigned long long* MP, const unsigned int* MPL, int64_t ntiles, int64_t mp_ld,
+                             int d,
+                             unsigned long long* mom, const unsigned int* flags, hipStream_t st,
+                             const unsigned int* abort);
+// the chains' states after a block from the int16 history of the block's Klein launch:
+// zs[c] = proposal fsel[c] (kept as is when fsel[c] < 0); history [d / 16][lanes][16] of z + 128
+hipError_t final_h16(const int16_t* h16, int64_t lanes, const int64_t* fsel, int64_t nc, int d, void* zs,
+                     int ob, int zs_cm, hipStream_t st, const unsigned int* abort);
 // VNP (nullable, 2 ceil(d / 128) x vn_n): per-(half coordinate tile, row) partial sums of
 // ||v||^2 of rows q < vn_n (bz_i8), summed per row into VN by vnorm2_reduce (n = vn_n)
 hipError_t vnorm2_reduce(const double* VNP, int d, int64_t n, int64_t rb, int64_t rstride, int64_t roff,

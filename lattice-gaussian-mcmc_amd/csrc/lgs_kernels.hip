@@ -2203,7 +2203,7 @@ __global__ __launch_bounds__(64) void imhk_accept_cert_kernel(const AcceptArgs a
 // RY coordinates per workgroup (vector path): the weights cnt and the chains'
 // final-state indices are loaded once for RY rows of the store instead of once
 // per row (they were 2-3x the coefficient bytes per row, from L2).
-template <typename ZT, typename OT, bool VEC, int RY = 1>
+template <typename ZT, typename OT, bool VEC, int RY = 1, bool GS = false>
 __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict__ Z, int64_t ldz,
                                                             const int32_t* __restrict__ cnt, int64_t n,
                                                             int64_t T, const int64_t* __restrict__ fsel,
@@ -2212,10 +2212,10 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
                                                             OT* __restrict__ zs, int zs_cm, int64_t nc,
                                                             const unsigned int* abort,
                                                             const uint8_t* __restrict__ znz, int64_t zlanes,
-                                                            int zshift) {
-    if (aborted(abort)) return;
-    const int i0 = blockIdx.y * RY;
-    const int64_t p0 = (int64_t)blockIdx.x * chunk;
+                                                            int zshift, const unsigned int* need) {
+    if (aborted(abort) || not_needed(need)) return;
+    __shared__ long long r1[RY][4], r2[RY][4];
+    auto tile = [&](const int i0, const int64_t p0) {
     const int64_t p1 = p0 + chunk < n ? p0 + chunk : n;
     long long s1[RY], s2[RY];
 #pragma unroll
@@ -2297,7 +2297,6 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
         }
     }
     // wave sums by shuffles, then the 4 waves' partials through LDS
-    __shared__ long long r1[RY][4], r2[RY][4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int r = 0; r < RY; ++r) {
@@ -2318,6 +2317,18 @@ __global__ __launch_bounds__(256) void moments_final_kernel(const ZT* __restrict
         atomicAdd(mom + i0 + r, (unsigned long long)(r1[r][0] + r1[r][1] + r1[r][2] + r1[r][3]));
         atomicAdd(mom + d + i0 + r, (unsigned long long)(r2[r][0] + r2[r][1] + r2[r][2] + r2[r][3]));
     }
+    };
+    if constexpr (GS) {  // grid-strided: the gated fallback after B z's moments launches a small grid
+        const int64_t nbx = (n + chunk - 1) / chunk;
+        const int nby = (d + RY - 1) / RY;
+        for (int by = blockIdx.y; by < nby; by += gridDim.y)
+            for (int64_t bx = blockIdx.x; bx < nbx; bx += gridDim.x) {
+                tile(by * RY, bx * chunk);
+                __syncthreads();  // (r1 / r2 reused by the next tile)
+            }
+    } else {
+        tile(blockIdx.y * RY, (int64_t)blockIdx.x * chunk);
+    }
 }
 
 // Carried-in states (row-major or coordinate-major z_state) weighted by cnt_carry.
@@ -2326,9 +2337,10 @@ __global__ __launch_bounds__(256) void moments_carry_kernel(const ZT* __restrict
                                                             int coord_major, int64_t nc, int d,
                                                             const int32_t* __restrict__ cc,
                                                             unsigned long long* mom,
-                                                            const unsigned int* abort) {
-    if (aborted(abort)) return;
-    const int i = blockIdx.x;
+                                                            const unsigned int* abort,
+                                                            const unsigned int* need) {
+    if (aborted(abort) || not_needed(need)) return;
+    for (int i = blockIdx.x; i < d; i += gridDim.x) {
     long long s1 = 0, s2 = 0;
     for (int64_t c = threadIdx.x; c < nc; c += blockDim.x) {
         const long long w = cc[c];
@@ -2351,6 +2363,8 @@ __global__ __launch_bounds__(256) void moments_carry_kernel(const ZT* __restrict
     if (threadIdx.x == 0) {
         atomicAdd(mom + i, (unsigned long long)r1[0]);
         atomicAdd(mom + d + i, (unsigned long long)r2[0]);
+    }
+    __syncthreads();  // (r1 / r2 reused by the next strided coordinate)
     }
 }
 
@@ -2577,7 +2591,7 @@ typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v16i_t __attribute__((ext_vector_type(16)));
 
 #ifndef LGS_BZ_OCC
-#define LGS_BZ_OCC 2
+#define LGS_BZ_OCC 3  // (round 5: pinned to three workgroups per CU; unpinned the int32 store instantiation drifted to 174 VGPRs)
 #endif
 #ifndef LGS_BZ_TXPER
 #define LGS_BZ_TXPER 1
@@ -2599,7 +2613,9 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
                                                     int64_t hcols, const unsigned int* abort,
                                                     const uint8_t* __restrict__ znz,
                                                     const unsigned int* __restrict__ clive, int64_t clive_ld,
-                                                    double* __restrict__ VNP, int64_t vn_n) {
+                                                    double* __restrict__ VNP, int64_t vn_n,
+                                                    unsigned long long* __restrict__ MP, int64_t mp_ld,
+                                                    unsigned int* __restrict__ MPL) {
     if (aborted(abort)) return;  // (whole grid) the selections were not written
     constexpr int TA = LGS_BZ_TA;  // 32-sample MFMA tiles per wave
     constexpr int BM = 64 * TA, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
@@ -2702,21 +2718,29 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
             }
         }
     }
+    // (MP) the tile's live-chunk words for the moments' reduction: a chunk the tile
+    // skips leaves its partials unwritten
+    if (MP != nullptr && use_clive && tx == 0 && tid < ngw) MPL[(size_t)ty * ngw + tid] = ngw == 1 ? live1 : livew4[0][tid];
     if (use_znz) {
         const bool hp = zs_ < n && zcol < hcols;
         for (int w = tid; w < (ci1 - ci0 + 31) / 32; w += 256) livew[w] = 0u;
         __syncthreads();
         for (int ci = ci0; ci < ci1; ++ci) {
-            const int c0 = kchunk[ci] * KC;
+            const int c0 = (kchunk[ci] & 0xffff) * KC;
             const bool nz = zs_ < n && (!hp || znz[(size_t)((c0 + zq * 16) >> 4) * h16_lanes + zcol] != 0);
             if (nz) atomicOr(&livew[(ci - ci0) >> 5], 1u << ((ci - ci0) & 31));
         }
         __syncthreads();
     }
     for (int ci = ci0; ci < ci1; ++ci) {
-        const int cix = kchunk[ci];
-        if (use_clive && !(((ngw == 1 ? live1 : livew4[wave][cix >> 5]) >> (cix & 31)) & 1u)) continue;  // (uniform)
-        if (use_znz && !((livew[(ci - ci0) >> 5] >> ((ci - ci0) & 31)) & 1u)) continue;  // (uniform)
+        // (bit 16 of a chunk entry: this row tile owns the chunk's moments, MP)
+        const int kraw = kchunk[ci];
+        const int cix = kraw & 0xffff;
+        const bool mown = MP != nullptr && (kraw >> 16) != 0 && KPT == 16;
+        if ((use_clive && !(((ngw == 1 ? live1 : livew4[wave][cix >> 5]) >> (cix & 31)) & 1u)) ||
+            (use_znz && !((livew[(ci - ci0) >> 5] >> ((ci - ci0) & 31)) & 1u))) {  // (uniform)
+            continue;  // (an all-zero chunk's moment partials stay 0: MP is cleared per launch)
+        }
         const int c0 = cix * KC;
         if (KPT == 16 && h16 != nullptr && zs_ < n && zcol < hcols) {
             // column written by the Klein launch whose int16 history (z + 128,
@@ -2775,6 +2799,35 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
             *(v4i_t*)&Bs0[row * P + part * 16] = *(const v4i_t*)&Bd0[g];
         }
         __syncthreads();
+        if (mown) {
+            // (round 5) the kept states' moments ride on this tile's digit planes while the
+            // MFMAs run: wave w sums coordinates 16w..16w+15 of the chunk over the tile's 64
+            // rows, lane (4 coordinates: lane & 3) x (4 rows: lane >> 2), packed per row as
+            // z^2 * 2^24 + (z + 32768) (64 rows: the low field < 2^22, the total < 2^63;
+            // rows past n hold z = 0 and add the bias only), then across the 16 lane groups
+            const int kk = 16 * wave + 4 * (lane & 3);
+            unsigned long long ps[4] = {0ull, 0ull, 0ull, 0ull};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = 4 * (lane >> 2) + i;
+                const unsigned int lo4 = *(const unsigned int*)&Zs0[row * P + kk];
+                const unsigned int hi4 = *(const unsigned int*)&Zs1[row * P + kk];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int z = 256 * (int)(signed char)(hi4 >> (8 * j)) + (int)(signed char)(lo4 >> (8 * j));
+                    ps[j] += ((unsigned long long)(unsigned int)(z * z) << 24) + (unsigned int)(z + 32768);
+                }
+            }
+#pragma unroll
+            for (int o = 4; o < 64; o <<= 1)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) ps[j] += __shfl_xor(ps[j], o);
+            if (lane < 4) {
+                unsigned long long* mp = MP + (size_t)ty * mp_ld + c0 + kk;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) mp[j] = ps[j];
+            }
+        }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int kb = ks * 32 + 16 * (lane >> 5);
@@ -2898,6 +2951,63 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
     }
     }
     if (zmax > (ZT)32639 || zmin < (ZT)-32639) atomicOr(flags, kFlagI8Range);
+}
+
+// Moments of the kept states from bz_i8_kernel's partials: column sums over the tiles
+// of the packed words, unpacked per word (the low 24 bits less the 64-row bias: sum z;
+// the rest: sum z^2), exact in int64; the tile's live-chunk words (MPL) mark the
+// chunks it skipped (no word written).  Skipped when the digit-range flag is up (a
+// carried |z| beyond two digits: the gated moments pass recomputes them then).
+__global__ __launch_bounds__(256) void bz_moments_reduce_kernel(const unsigned long long* __restrict__ MP,
+                                                                const unsigned int* __restrict__ MPL,
+                                                                int64_t ntiles, int64_t mp_ld, int d,
+                                                                int64_t per, unsigned long long* mom,
+                                                                const unsigned int* flags,
+                                                                const unsigned int* abort) {
+    if (aborted(abort) || (flags && (*(const volatile unsigned int*)flags & kFlagI8Range))) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= d) return;
+    const int64_t t0 = (int64_t)blockIdx.y * per, t1 = min<int64_t>(t0 + per, ntiles);
+    const int ngw = (d + 2047) / 2048;
+    long long s1 = 0, s2 = 0;
+    for (int64_t t = t0; t < t1; ++t) {
+        if (!((MPL[(size_t)t * ngw + (i >> 11)] >> ((i >> 6) & 31)) & 1u)) continue;  // chunk all-zero in the tile
+        const unsigned long long w = MP[(size_t)t * mp_ld + i];
+        s1 += (long long)(w & 0xffffffull) - 64ll * 32768ll;
+        s2 += (long long)(w >> 24);
+    }
+    atomicAdd(mom + i, (unsigned long long)s1);
+    atomicAdd(mom + d + i, (unsigned long long)s2);
+}
+
+// The chains' states after a block, from the int16 history (z + 128, 16 coordinates
+// of a proposal in 32 contiguous bytes) instead of the coordinate-major store (one
+// 2-byte element per 64-byte line there).  Thread per (chain, 16-coordinate block),
+// chain fastest.
+template <typename OT>
+__global__ __launch_bounds__(256) void final_h16_kernel(const int16_t* __restrict__ h16, int64_t lanes,
+                                                        const int64_t* __restrict__ fsel, int64_t nc, int d,
+                                                        OT* __restrict__ zs, int zs_cm,
+                                                        const unsigned int* abort) {
+    if (aborted(abort)) return;
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= nc) return;
+    const int64_t p = fsel[c];
+    if (p < 0) return;  // no proposal accepted in the block: the carried state stays
+    const int b = blockIdx.y;
+    const v4u_t* hp = (const v4u_t*)(h16 + ((size_t)b * lanes + p) * 16);
+    const v4u_t y0 = hp[0], y1 = hp[1];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int i = 16 * b + j;
+        if (i >= d) break;
+        const unsigned int wv = j < 8 ? y0[j >> 1] : y1[(j - 8) >> 1];
+        const OT z = (OT)((int)(short)(wv >> (16 * (j & 1))) - 128);
+        if (zs_cm)
+            zs[(size_t)i * nc + c] = z;
+        else
+            zs[(size_t)c * d + i] = z;
+    }
 }
 
 // Coefficient k of each kept state (a scalar functional for lag sums):
@@ -3116,7 +3226,7 @@ hipError_t accept(const AcceptArgs& a, const KleinArgs& ka, hipStream_t st) {
 hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt, int64_t n, int64_t T,
                          const int64_t* fsel, int d, unsigned long long* mom, void* zs, int ob,
                          int zs_cm, int64_t nc, hipStream_t st, const unsigned int* abort,
-                         const uint8_t* znz, int64_t zlanes, int zshift) {
+                         const uint8_t* znz, int64_t zlanes, int zshift, const unsigned int* need) {
     if (n <= 0) return hipSuccess;
     if (zb != 2 || zlanes % 8 != 0) znz = nullptr;  // (8 proposals per flag load, 16-bit store only)
 #ifdef LGS_MOM_NO_ZNZ
@@ -3127,25 +3237,35 @@ hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt,
 #define LGS_MOM_RY 4
 #endif
     constexpr int RY = LGS_MOM_RY;  // rows per workgroup, vector path
-    const dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
-    const dim3 gridv((unsigned)((n + chunk - 1) / chunk), (unsigned)((d + RY - 1) / RY));
+    dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
+    dim3 gridv((unsigned)((n + chunk - 1) / chunk), (unsigned)((d + RY - 1) / RY));
+    if (need) {  // gated fallback: a small grid that returns at once unless needed
+        grid.x = gridv.x = std::min(grid.x, 8u);
+        grid.y = std::min(grid.y, 32u);
+        gridv.y = std::min(gridv.y, 32u);
+    }
     const int vw = zb == 2 ? 8 : 4;  // proposals per lane of the vector path
     const bool vec = ldz % vw == 0 && n % vw == 0 && ((uintptr_t)Z % (vw * (uintptr_t)zb)) == 0 &&
                      (!cnt || ((uintptr_t)cnt % 16) == 0);
     LGS_ZT(zb, ZT, LGS_ZT(ob, OT, {
-        if (vec)
-            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, true, RY>), gridv, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort, znz, zlanes, zshift);
+        if (vec && need)
+            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, true, RY, true>), gridv, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort, znz, zlanes, zshift, need);
+        else if (vec)
+            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, true, RY>), gridv, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort, znz, zlanes, zshift, need);
+        else if (need)
+            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, false, 1, true>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort, (const uint8_t*)nullptr, (int64_t)0, 0, need);
         else
-            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, false>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort, (const uint8_t*)nullptr, (int64_t)0, 0);
+            hipLaunchKernelGGL((moments_final_kernel<ZT, OT, false>), grid, dim3(256), 0, st, (const ZT*)Z, ldz, cnt, n, T, fsel, d, chunk, mom, (OT*)zs, zs_cm, nc, abort, (const uint8_t*)nullptr, (int64_t)0, 0, need);
     }));
     return hipGetLastError();
 }
 
 hipError_t moments_carry(const void* zs, int zb, int coord_major, int64_t nc, int d,
                          const int32_t* cc, unsigned long long* mom, hipStream_t st,
-                         const unsigned int* abort) {
+                         const unsigned int* abort, const unsigned int* need) {
     if (nc <= 0) return hipSuccess;
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(moments_carry_kernel<ZT>, dim3(d), dim3(256), 0, st, (const ZT*)zs, coord_major, nc, d, cc, mom, abort));
+    const unsigned gx = need ? (unsigned)std::min(d, 64) : (unsigned)d;  // (gated: small grid)
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(moments_carry_kernel<ZT>, dim3(gx), dim3(256), 0, st, (const ZT*)zs, coord_major, nc, d, cc, mom, abort, need));
     return hipGetLastError();
 }
 
@@ -3292,7 +3412,8 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
                  double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
                  unsigned int* flags, const int16_t* h16, int64_t h16_lanes, int64_t hcols,
                  hipStream_t st, const unsigned int* abort, const uint8_t* znz, const unsigned int* clive,
-                 int64_t clive_ld, double* VNP, int64_t vn_n) {
+                 int64_t clive_ld, double* VNP, int64_t vn_n, unsigned long long* MP, int64_t mp_ld,
+                 unsigned int* MPL) {
     if (n <= 0) return hipSuccess;
     if (vn_n <= 0) VNP = nullptr;
     if (d % 16 != 0 || LGS_BZ_TA != 1 || d > kOzMaxD) h16 = nullptr;  // history blocks must align with the chunks
@@ -3313,7 +3434,27 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
     const int tx = ((d + 127) / 128 + LGS_BZ_TXPER - 1) / LGS_BZ_TXPER;  // coordinate-tile groups
     const int64_t ty = (n + 64 * LGS_BZ_TA - 1) / (64 * LGS_BZ_TA);
     const dim3 grid((unsigned)(tx * ((ty + 7) / 8) * 8));  // whole rounds of 8 XCDs (extra tiles exit)
-    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort, znz, clive, clive_ld, VNP, vn_n));
+    LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort, znz, clive, clive_ld, VNP, vn_n, MP, mp_ld, MPL));
+    return hipGetLastError();
+}
+
+hipError_t bz_moments_reduce(const unsigned long long* MP, const unsigned int* MPL, int64_t ntiles, int64_t mp_ld,
+                             int d, unsigned long long* mom, const unsigned int* flags, hipStream_t st,
+                             const unsigned int* abort) {
+    if (ntiles <= 0) return hipSuccess;
+    const int64_t per = 128;  // tiles per workgroup
+    const dim3 grid((unsigned)((d + 255) / 256), (unsigned)((ntiles + per - 1) / per));
+    hipLaunchKernelGGL(bz_moments_reduce_kernel, grid, dim3(256), 0, st, MP, MPL, ntiles, mp_ld, d, per, mom,
+                       flags, abort);
+    return hipGetLastError();
+}
+
+hipError_t final_h16(const int16_t* h16, int64_t lanes, const int64_t* fsel, int64_t nc, int d, void* zs,
+                     int ob, int zs_cm, hipStream_t st, const unsigned int* abort) {
+    if (nc <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((nc + 255) / 256), (unsigned)((d + 15) / 16));
+    LGS_ZT(ob, OT, hipLaunchKernelGGL(final_h16_kernel<OT>, grid, dim3(256), 0, st, h16, lanes, fsel, nc, d,
+                                      (OT*)zs, zs_cm, abort));
     return hipGetLastError();
 }
 

@@ -309,6 +309,7 @@ def _imhk_carried(capi, on_caller_stream: bool, zmax: int):
     lw = torch.full((nc,), 1e300, dtype=torch.float64, device=dev)
     init = torch.ones(nc, dtype=torch.int32, device=dev)
     acc = torch.zeros(nc, dtype=torch.int64, device=dev)
+    mom = torch.zeros(2 * d, dtype=torch.int64, device=dev)
     vs = torch.zeros((nc, steps, d), dtype=torch.float64, device=dev)
     vn2 = torch.zeros((nc, steps), dtype=torch.float64, device=dev)
     zk = torch.zeros((nc, steps), dtype=torch.int64, device=dev)
@@ -324,12 +325,12 @@ def _imhk_carried(capi, on_caller_stream: bool, zmax: int):
     s = torch.cuda.Stream(device=dev)
     if on_caller_stream:  # lgs_set_stream: the call's early check applies
         ctx.set_stream(s.cuda_stream)
-    ctx.imhk(5, 0, nc, 1, steps, 1, z, lw, init, acc, v_samples=vs, vnorm2_samples=vn2, zk_samples=zk,
-             zk_index=3, flags=capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR,
+    ctx.imhk(5, 0, nc, 1, steps, 1, z, lw, init, acc, v_samples=vs, moments=mom, vnorm2_samples=vn2,
+             zk_samples=zk, zk_index=3, flags=capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR,
              lag=(L, zr, zsum, vr, vsum, 1e-6))
     torch.cuda.synchronize()
-    out = {k: t.cpu().numpy() for k, t in dict(z=z, acc=acc, v=vs, vn2=vn2, zk=zk, zsum=zsum, vsum=vsum,
-                                                 zr=zr, vr=vr).items()}
+    out = {k: t.cpu().numpy() for k, t in dict(z=z, acc=acc, mom=mom, v=vs, vn2=vn2, zk=zk, zsum=zsum,
+                                                 vsum=vsum, zr=zr, vr=vr).items()}
     ctx.close()
     return z0, B, out
 
@@ -346,6 +347,10 @@ def test_early_check_equals_synchronised_call(capi, zmax):
     for k in a:
         assert np.array_equal(a[k], b[k]), k
     assert not a["acc"].any()
+    # moments of the 6 kept states per chain (all the carried one): on the caller's stream
+    # from B z's digit tiles, or (|z| beyond two digits) from the gated moments pass
+    z64 = z0.astype(np.int64)
+    assert np.array_equal(a["mom"], np.concatenate([6 * z64.sum(1), 6 * (z64 ** 2).sum(1)]))
     want = (B.astype(np.int64) @ z0.astype(np.int64)).T  # nc x d
     # ||v||^2 reaches ~1e20 at |z| ~ 32639 (beyond 2^53: fp64 sums in another order than
     # numpy's), so against numpy to rounding; the early-checked and host-checked calls
