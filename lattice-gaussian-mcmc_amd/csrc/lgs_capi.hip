@@ -178,6 +178,22 @@ struct lgs_ctx {
     int bset_next = 0;
     hipStream_t kstream = nullptr;
     hipEvent_t ev_klein = nullptr;
+    // Look-ahead: at the end of a pipelined call, the Klein launch of the next call's
+    // first block as this call predicts it (same seed, chains, steps per call, store;
+    // the counters continue) is enqueued on kstream into the next set, so the Klein
+    // stream never waits for the host's turnaround between calls.  The next call uses
+    // it when its first block matches the prediction, else discards it (it writes
+    // only that set).  Proposals are counter-addressed: a launch made early is the
+    // same launch.
+    struct Spec {
+        bool valid = false;
+        uint64_t seed = 0, chain0 = 0, step0 = 0;
+        int64_t nc = 0, Tb = 0, ldzb = 0;
+        int zb = 0, j = 0;
+        bool wl = false, exact = false, oz = false;
+        decltype(hist) h;
+        hipEvent_t ev = nullptr;  // recorded on kstream behind the launch
+    } spec;
 };
 
 namespace {
@@ -256,6 +272,16 @@ struct SetSwap {
     }
     ~SetSwap() { restore(); }
 };
+
+// Drops a look-ahead Klein launch (lgs_ctx::Spec): waits for it and clears the flag
+// words it wrote into its set.
+int spec_discard(lgs_ctx* c) {
+    if (!c->spec.valid) return LGS_OK;
+    c->spec.valid = false;
+    HIP_TRY(hipStreamSynchronize(c->kstream));
+    HIP_TRY(hipMemset(c->bset[c->spec.j].flags.p, 0, 4 * lgs::kFlagWords));
+    return LGS_OK;
+}
 
 // Wait for the stream; if an int8-digit B z saw a coefficient beyond two digits,
 // replay the pending B z launches with the fp64 kernel.  Must run before any
@@ -720,6 +746,7 @@ int lgs_destroy(lgs_ctx* c) {
         (void)hipStreamDestroy(c->kstream);
     }
     if (c->ev_klein) (void)hipEventDestroy(c->ev_klein);
+    if (c->spec.ev) (void)hipEventDestroy(c->spec.ev);
     for (auto& s : c->bset)
         if (s.ev_free) (void)hipEventDestroy(s.ev_free);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -734,7 +761,7 @@ int lgs_set_stream(lgs_ctx* c, void* s) {
     // the old stream may still run an early-checked lgs_imhk's later launches, which
     // read the context's buffers: finish them before another stream reuses those
     if (ns != c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->kstream) HIP_TRY(hipStreamSynchronize(c->kstream));
+    if (c->kstream) HIP_TRY(hipStreamSynchronize(c->kstream));  // (a look-ahead launch stays valid)
     c->stream = ns;
     return LGS_OK;
 }
@@ -753,6 +780,7 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     // context's stream and read R, BT, the digit planes, records, EMAX: the blocking
     // copies below are not ordered after a non-blocking stream's work
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if ((rc = spec_discard(c))) return rc;  // (a look-ahead launch reads the basis being replaced)
     const int PB = c->panel;
     const size_t dd = (size_t)d;
     // per-coordinate parameters (klein.py:195-211, 255-263)
@@ -1375,6 +1403,17 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
                 return rc;
         }
     }
+    // the previous call's look-ahead launch: this call's first block if it matches
+    static const bool no_look = getenv("LGS_NO_LOOKAHEAD") && atoi(getenv("LGS_NO_LOOKAHEAD")) == 1;
+    bool spec_hit = false;
+    if (c->spec.valid) {
+        const int64_t tb0 = std::min<int64_t>(T, n_steps);
+        const auto& sp = c->spec;
+        spec_hit = pipe && sp.seed == seed && sp.chain0 == first_chain && sp.step0 == first_step && sp.nc == nc &&
+                   sp.Tb == tb0 && sp.ldzb == nc * tb0 + (carry ? nc : 0) && sp.zb == zb && sp.wl == wl &&
+                   sp.exact == exact && sp.j == c->bset_next;
+        if (!spec_hit && (rc = spec_discard(c))) return rc;
+    }
     if ((rc = c->Z.reserve((size_t)own_cols * d * std::max(zb, 4))) ||
         (rc = c->LW.reserve((size_t)(pipe ? nc : np) * 8)) ||
         (rc = c->sel.reserve((size_t)std::max<int64_t>(nc * kmax, nc) * 8)) ||
@@ -1481,7 +1520,13 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             a.emax = c->EMAX.as<unsigned long long>();
         }
         bool ozb = false;
-        if (pipe) {  // on kstream, once the set's last reader (two blocks back) is done
+        if (pipe && spec_hit && t0 == 0) {  // the previous call's look-ahead launch is this block's
+            spec_hit = false;
+            c->spec.valid = false;
+            ozb = c->spec.oz;
+            c->hist = c->spec.h;
+            HIP_TRY(hipStreamWaitEvent(c->stream, c->spec.ev, 0));
+        } else if (pipe) {  // on kstream, once the set's last reader (two blocks back) is done
             auto& bs = c->bset[sw.j];
             if (bs.free_recorded) HIP_TRY(hipStreamWaitEvent(c->kstream, bs.ev_free, 0));
             const hipStream_t cs = c->stream;
@@ -1656,6 +1701,51 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
         }
         if (redo) continue;  // same block again (block 0: its initial draws too)
         t0 += T;
+    }
+    // the next call's first block as this call predicts it (same arguments, counters
+    // continued), on kstream into the next set behind this call's last Klein launch
+    const uint64_t next_step = first_step + (uint64_t)n_steps;
+    if (pipe && !no_look && next_step + (uint64_t)n_steps <= (1ull << 32)) {
+        const int j = c->bset_next;
+        SetSwap sw;
+        sw.c = c;
+        sw.j = j;
+        sw.swap_flags();
+        sw.swap_store();
+        const int64_t tb0 = std::min<int64_t>(T, n_steps), ldz0 = nc * tb0 + (carry ? nc : 0);
+        lgs::KleinArgs a = base_args(c, seed);
+        a.counter_mode = 1;
+        a.chain0 = (uint32_t)first_chain;
+        a.step0 = (uint32_t)next_step;
+        a.nt = tb0;
+        a.n = nc * tb0;
+        a.ldz = ldz0;
+        a.LW = c->LW.as<double>();
+        auto& bs = c->bset[j];
+        if (bs.free_recorded) HIP_TRY(hipStreamWaitEvent(c->kstream, bs.ev_free, 0));
+        const hipStream_t cs = c->stream;
+        c->stream = c->kstream;
+        int zbs = zb;
+        bool oz = false;
+        rc = run_klein_store(c, a, exact, wl, zbs, c->Z.p, true, &oz);
+        c->stream = cs;
+        if (rc) return rc;
+        if (!c->spec.ev) HIP_TRY(hipEventCreateWithFlags(&c->spec.ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->spec.ev, c->kstream));
+        auto& sp = c->spec;
+        sp.valid = true;
+        sp.seed = seed;
+        sp.chain0 = first_chain;
+        sp.step0 = next_step;
+        sp.nc = nc;
+        sp.Tb = tb0;
+        sp.ldzb = ldz0;
+        sp.zb = zb;
+        sp.j = j;
+        sp.wl = wl;
+        sp.exact = exact;
+        sp.oz = oz;
+        sp.h = c->hist;
     }
     if (!dev) {
         HIP_TRY(hipMemcpyAsync(z_state, zs, (size_t)nc * d * ob, hipMemcpyDeviceToHost, c->stream));
@@ -2196,6 +2286,7 @@ int lgs_set_decoder(lgs_ctx* c, const double* Q, const double* Binv) {
     const int64_t d = c->d;
     const size_t bytes = (size_t)d * d * 8;
     HIP_TRY(hipStreamSynchronize(c->stream));  // (as lgs_set_basis: in-flight work may read the buffers)
+    if (c->kstream) HIP_TRY(hipStreamSynchronize(c->kstream));
     if (Q) {
         if ((rc = c->DQ.reserve(bytes))) return rc;
         HIP_TRY(hipMemcpy(c->DQ.p, Q, bytes, hipMemcpyHostToDevice));  // gemm_f64 reads Q[c][r]

@@ -372,7 +372,7 @@ def test_early_check_equals_synchronised_call(capi, zmax):
             np.testing.assert_allclose(got, w, rtol=1e-12, atol=0)
 
 
-def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, blocks: int = 3):
+def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, blocks: int = 3, plan=None):
     """Several lgs_imhk_ex calls of several blocks each (LGS_MAX_PROPOSALS: T = 4 steps
     per block), chain state, accept counts, moments, lattice points, functionals and
     lag sums carried across them -- on a caller's stream the blocks are pipelined
@@ -394,7 +394,7 @@ def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, 
             os.environ["LGS_MAX_PROPOSALS"] = old
     ctx.set_basis(R, cp, B, float(g["sigma"]))
     dev = "cuda:0"
-    steps = T * blocks
+    plan = plan or [T * blocks] * calls  # steps per call (a changed count discards the look-ahead launch)
     z = torch.zeros((d, nc), dtype=torch.int32, device=dev)
     lw = torch.zeros(nc, dtype=torch.float64, device=dev)
     init = torch.zeros(nc, dtype=torch.int32, device=dev)
@@ -411,14 +411,16 @@ def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, 
         ctx.set_stream(s.cuda_stream)
     vs_all, vn_all, zk_all = [], [], []
     with torch.cuda.stream(s):
-        for call in range(calls):
+        first = 1
+        for steps in plan:
             vs = torch.zeros((nc, steps, d), dtype=torch.float64, device=dev)
             vn2 = torch.zeros((nc, steps), dtype=torch.float64, device=dev)
             zk = torch.zeros((nc, steps), dtype=torch.int64, device=dev)
-            ctx.imhk(11, 0, nc, 1 + call * steps, steps, 1, z, lw, init, acc, v_samples=vs, moments=mom,
+            ctx.imhk(11, 0, nc, first, steps, 1, z, lw, init, acc, v_samples=vs, moments=mom,
                      vnorm2_samples=vn2, zk_samples=zk, zk_index=5,
                      flags=capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR | flags_extra,
                      lag=(L, zr, zsum, vr, vsum, 1e-6))
+            first += steps
             vs_all.append(vs)
             vn_all.append(vn2)
             zk_all.append(zk)
@@ -432,15 +434,17 @@ def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, 
     return B, out
 
 
-@pytest.mark.parametrize("mode", ["reference", "wang_ling_exact"])
-def test_pipelined_blocks_equal_synchronised_calls(capi, mode):
+@pytest.mark.parametrize("mode,plan", [("reference", None), ("wang_ling_exact", None), ("reference", [12, 4, 4, 8])])
+def test_pipelined_blocks_equal_synchronised_calls(capi, mode, plan):
     """Pipelined blocks (caller's stream) give every output of the host-checked calls
-    on the library's own stream, bit for bit, over 3 calls x 3 blocks; v is B z of the
-    kept states (z_k recovered from v through the basis' inverse is checked against
-    zk)."""
+    on the library's own stream, bit for bit, over 3 calls x 3 blocks (each call's
+    first block from the previous call's look-ahead launch), or calls of 3, 1, 1 and 2
+    blocks (a look-ahead discarded on the changed step count, used on the repeated
+    one); v is B z of the kept states (z_k recovered from v through the basis' inverse
+    is checked against zk)."""
     fx = 0 if mode == "reference" else capi.LGS_WANG_LING | capi.LGS_EXACT_ORDER
-    B, a = _imhk_calls(capi, True, fx)
-    _, b = _imhk_calls(capi, False, fx)
+    B, a = _imhk_calls(capi, True, fx, plan=plan)
+    _, b = _imhk_calls(capi, False, fx, plan=plan)
     for k in a:
         assert np.array_equal(a[k], b[k]), k
     steps = a["v"].shape[1]
