@@ -174,8 +174,10 @@ struct lgs_ctx {
         DevBuf Z, LW, H16, ZNZ, CLIVE, flags;
         hipEvent_t ev_free = nullptr;
         bool free_recorded = false;
-    } bset[2];
+    } bset[3];
     int bset_next = 0;
+    int nsets = 2;  // buffer sets in rotation (LGS_PIPE_SETS=3: three, fixed at the first pipelined call)
+    bool kstream_sets_fixed = false;
     hipStream_t kstream = nullptr;
     hipEvent_t ev_klein = nullptr;
     // Look-ahead: at the end of a pipelined call, the Klein launch of the next call's
@@ -632,6 +634,58 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
         return LGS_OK;
     }
     c->pending_i8.push_back(b);
+    return LGS_OK;
+}
+
+// The look-ahead launch (lgs_ctx::Spec): the next call's first block as this call
+// predicts it (same arguments, step counter continued), on kstream into set j --
+// right behind the call's last Klein launch, before the call waits for anything, so
+// the Klein stream runs back to back.  The context's working buffers, history and
+// stream are restored on return.
+int lookahead(lgs_ctx* c, int j, uint64_t seed, uint64_t first_chain, uint64_t step0, int64_t nc, int64_t tb,
+              bool carry, int zb, bool exact, bool wl) {
+    const auto hist = c->hist;
+    SetSwap sw;
+    sw.c = c;
+    sw.j = j;
+    sw.swap_flags();
+    sw.swap_store();
+    const int64_t ldz = nc * tb + (carry ? nc : 0);
+    lgs::KleinArgs a = base_args(c, seed);
+    a.counter_mode = 1;
+    a.chain0 = (uint32_t)first_chain;
+    a.step0 = (uint32_t)step0;
+    a.nt = tb;
+    a.n = nc * tb;
+    a.ldz = ldz;
+    a.LW = c->LW.as<double>();
+    auto& bs = c->bset[j];
+    if (bs.free_recorded) HIP_TRY(hipStreamWaitEvent(c->kstream, bs.ev_free, 0));
+    const hipStream_t cs = c->stream;
+    c->stream = c->kstream;
+    int zbs = zb;
+    bool oz = false;
+    const int rc = run_klein_store(c, a, exact, wl, zbs, c->Z.p, true, &oz);
+    c->stream = cs;
+    const auto h = c->hist;
+    c->hist = hist;
+    if (rc) return rc;
+    if (!c->spec.ev) HIP_TRY(hipEventCreateWithFlags(&c->spec.ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->spec.ev, c->kstream));
+    auto& sp = c->spec;
+    sp.valid = true;
+    sp.seed = seed;
+    sp.chain0 = first_chain;
+    sp.step0 = step0;
+    sp.nc = nc;
+    sp.Tb = tb;
+    sp.ldzb = ldz;
+    sp.zb = zb;
+    sp.j = j;
+    sp.wl = wl;
+    sp.exact = exact;
+    sp.oz = oz;
+    sp.h = h;
     return LGS_OK;
 }
 
@@ -1390,7 +1444,12 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
                 HIP_TRY(hipStreamCreateWithFlags(&c->kstream, hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&c->ev_klein, hipEventDisableTiming));
         }
-        for (auto& s : c->bset) {
+        if (!c->kstream_sets_fixed) {
+            c->nsets = getenv("LGS_PIPE_SETS") && atoi(getenv("LGS_PIPE_SETS")) == 3 ? 3 : 2;
+            c->kstream_sets_fixed = true;
+        }
+        for (int si = 0; si < c->nsets; ++si) {
+            auto& s = c->bset[si];
             if (!s.ev_free) HIP_TRY(hipEventCreateWithFlags(&s.ev_free, hipEventDisableTiming));
             if (!s.flags.p) {
                 if ((rc = s.flags.reserve(4 * lgs::kFlagWords))) return rc;
@@ -1465,6 +1524,13 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
     // per block (finish_or_redo).  A block whose Klein launch (or the chain states
     // carried into a 16-bit store) overflowed has its state-modifying dependants
     // skipped on the device (kAbortMask) and is redone at the wider width.
+    const uint64_t next_step = first_step + (uint64_t)n_steps;  // (the look-ahead's first step)
+    bool look_done = false;
+    // enqueued after the call's last wait (measured: 103.6-103.9 M samples/s against
+    // 101.7-102.9 M enqueued right behind the last Klein launch, whose dependants then
+    // start later and hold the next launch's set longer, profiles/r05u_bench_ab.log);
+    // LGS_LOOKAHEAD_EARLY=1: right behind it
+    static const bool look_late = !(getenv("LGS_LOOKAHEAD_EARLY") && atoi(getenv("LGS_LOOKAHEAD_EARLY")) == 1);
     for (int64_t t0 = 0; t0 < n_steps || t0 == 0;) {
         bool oz_used = false;
         SetSwap sw;  // (pipe) this block's buffer set, swapped back on every exit
@@ -1538,6 +1604,15 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_klein, 0));
         } else if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p, true, &ozb))) {
             return rc;
+        }
+        // (LGS_LOOKAHEAD_EARLY) the call's last block: the next call's first block as
+        // predicted, on kstream right behind this one (into the next set), before the wait
+        if (pipe && !no_look && !look_late && !look_done && t0 + T >= n_steps &&
+            next_step + (uint64_t)n_steps <= (1ull << 32)) {
+            look_done = true;
+            if ((rc = lookahead(c, (sw.j + 1) % c->nsets, seed, first_chain, next_step, nc, std::min<int64_t>(T, n_steps), carry,
+                                zb, exact, wl)))
+                return rc;
         }
         oz_used |= ozb;
         // chain states carried into the block's store (a state beyond 16 bits flags kFlagCarry16)
@@ -1697,56 +1772,15 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             fl = c->flags.as<unsigned int>();
             HIP_TRY(hipEventRecord(c->bset[j].ev_free, c->stream));
             c->bset[j].free_recorded = true;
-            if (!redo) c->bset_next ^= 1;
+            if (!redo) c->bset_next = (c->bset_next + 1) % c->nsets;
         }
         if (redo) continue;  // same block again (block 0: its initial draws too)
         t0 += T;
     }
-    // the next call's first block as this call predicts it (same arguments, counters
-    // continued), on kstream into the next set behind this call's last Klein launch
-    const uint64_t next_step = first_step + (uint64_t)n_steps;
-    if (pipe && !no_look && next_step + (uint64_t)n_steps <= (1ull << 32)) {
-        const int j = c->bset_next;
-        SetSwap sw;
-        sw.c = c;
-        sw.j = j;
-        sw.swap_flags();
-        sw.swap_store();
-        const int64_t tb0 = std::min<int64_t>(T, n_steps), ldz0 = nc * tb0 + (carry ? nc : 0);
-        lgs::KleinArgs a = base_args(c, seed);
-        a.counter_mode = 1;
-        a.chain0 = (uint32_t)first_chain;
-        a.step0 = (uint32_t)next_step;
-        a.nt = tb0;
-        a.n = nc * tb0;
-        a.ldz = ldz0;
-        a.LW = c->LW.as<double>();
-        auto& bs = c->bset[j];
-        if (bs.free_recorded) HIP_TRY(hipStreamWaitEvent(c->kstream, bs.ev_free, 0));
-        const hipStream_t cs = c->stream;
-        c->stream = c->kstream;
-        int zbs = zb;
-        bool oz = false;
-        rc = run_klein_store(c, a, exact, wl, zbs, c->Z.p, true, &oz);
-        c->stream = cs;
-        if (rc) return rc;
-        if (!c->spec.ev) HIP_TRY(hipEventCreateWithFlags(&c->spec.ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(c->spec.ev, c->kstream));
-        auto& sp = c->spec;
-        sp.valid = true;
-        sp.seed = seed;
-        sp.chain0 = first_chain;
-        sp.step0 = next_step;
-        sp.nc = nc;
-        sp.Tb = tb0;
-        sp.ldzb = ldz0;
-        sp.zb = zb;
-        sp.j = j;
-        sp.wl = wl;
-        sp.exact = exact;
-        sp.oz = oz;
-        sp.h = c->hist;
-    }
+    if (pipe && !no_look && look_late && next_step + (uint64_t)n_steps <= (1ull << 32))
+        if ((rc = lookahead(c, c->bset_next, seed, first_chain, next_step, nc, std::min<int64_t>(T, n_steps), carry, zb,
+                            exact, wl)))
+            return rc;
     if (!dev) {
         HIP_TRY(hipMemcpyAsync(z_state, zs, (size_t)nc * d * ob, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemcpyAsync(logw_state, lws, nc * 8, hipMemcpyDeviceToHost, c->stream));

@@ -2520,9 +2520,10 @@ __global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave & 1, wn = wave >> 1;
-    const int r0 = blockIdx.y * BN;
-    // sample tiles strided over the grid (one per workgroup except in the gated
-    // replay's small grid, which must not cost a full-size dispatch when not needed)
+    // row and sample tiles strided over the grid (one per workgroup except in the gated
+    // replay's small grid, which must not cost a full-size dispatch when not needed:
+    // beside a running Klein launch every workgroup waits for a free slot)
+    for (int r0 = blockIdx.y * BN; r0 < d; r0 += gridDim.y * BN)
     for (int64_t s0 = (int64_t)blockIdx.x * BM; s0 < n; s0 += (int64_t)gridDim.x * BM) {
     d4_t acc[2][2];
 #pragma unroll
@@ -3240,9 +3241,9 @@ hipError_t moments_final(const void* Z, int zb, int64_t ldz, const int32_t* cnt,
     dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)d);
     dim3 gridv((unsigned)((n + chunk - 1) / chunk), (unsigned)((d + RY - 1) / RY));
     if (need) {  // gated fallback: a small grid that returns at once unless needed
-        grid.x = gridv.x = std::min(grid.x, 8u);
-        grid.y = std::min(grid.y, 32u);
-        gridv.y = std::min(gridv.y, 32u);
+        grid.x = gridv.x = std::min(grid.x, 4u);
+        grid.y = std::min(grid.y, 4u);
+        gridv.y = std::min(gridv.y, 4u);
     }
     const int vw = zb == 2 ? 8 : 4;  // proposals per lane of the vector path
     const bool vec = ldz % vw == 0 && n % vw == 0 && ((uintptr_t)Z % (vw * (uintptr_t)zb)) == 0 &&
@@ -3264,7 +3265,7 @@ hipError_t moments_carry(const void* zs, int zb, int coord_major, int64_t nc, in
                          const int32_t* cc, unsigned long long* mom, hipStream_t st,
                          const unsigned int* abort, const unsigned int* need) {
     if (nc <= 0) return hipSuccess;
-    const unsigned gx = need ? (unsigned)std::min(d, 64) : (unsigned)d;  // (gated: small grid)
+    const unsigned gx = need ? (unsigned)std::min(d, 16) : (unsigned)d;  // (gated: small grid)
     LGS_ZT(zb, ZT, hipLaunchKernelGGL(moments_carry_kernel<ZT>, dim3(gx), dim3(256), 0, st, (const ZT*)zs, coord_major, nc, d, cc, mom, abort, need));
     return hipGetLastError();
 }
@@ -3317,7 +3318,7 @@ hipError_t vnorm2_rows(const double* V, int d, int64_t n, int64_t rb, int64_t rs
                        hipStream_t st, const unsigned int* abort, const unsigned int* need) {
     if (n <= 0) return hipSuccess;
     const int64_t nb = (n + 3) / 4;
-    hipLaunchKernelGGL(vnorm2_rows_kernel, dim3((unsigned)(need ? std::min<int64_t>(nb, 1024) : nb)), dim3(256), 0, st,
+    hipLaunchKernelGGL(vnorm2_rows_kernel, dim3((unsigned)(need ? std::min<int64_t>(nb, 16) : nb)), dim3(256), 0, st,
                        V, d, n, rb, rstride, roff, VN, abort, need);
     return hipGetLastError();
 }
@@ -3372,8 +3373,9 @@ hipError_t bz(const void* Z, int zb, int64_t ldz, const int64_t* sel, const doub
               int64_t n, double* V, int64_t ldv, int64_t rb, int64_t rstride, int64_t roff,
               hipStream_t st, const unsigned int* abort, const unsigned int* need) {
     if (n <= 0) return hipSuccess;
-    const int64_t nbx = (n + 63) / 64;  // (gated replay: 128 x-tiles, each workgroup loops)
-    const dim3 grid((unsigned)(need ? std::min<int64_t>(nbx, 128) : nbx), (unsigned)((d + 63) / 64));
+    const int64_t nbx = (n + 63) / 64;  // (gated replay: 4 x 4 workgroups, each loops)
+    const dim3 grid((unsigned)(need ? std::min<int64_t>(nbx, 4) : nbx),
+                    (unsigned)(need ? std::min(4, (d + 63) / 64) : (d + 63) / 64));
     LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_gemm_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, BT, d, n, V, ldv, rb, rstride, roff, abort, need));
     return hipGetLastError();
 }
