@@ -2591,6 +2591,14 @@ __global__ __launch_bounds__(256) void bz_gemm_kernel(const ZT* __restrict__ Z, 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v16i_t __attribute__((ext_vector_type(16)));
 
+// a 64-bit value rotated within each 16-lane DPP row (CTRL = 0x120 + r: row_ror:r)
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp_row_ror_u64(unsigned long long x) {
+    const unsigned int lo = (unsigned int)__builtin_amdgcn_update_dpp(0, (int)(unsigned int)x, CTRL, 0xf, 0xf, false);
+    const unsigned int hi = (unsigned int)__builtin_amdgcn_update_dpp(0, (int)(unsigned int)(x >> 32), CTRL, 0xf, 0xf, false);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 #ifndef LGS_BZ_OCC
 #define LGS_BZ_OCC 3  // (round 5: pinned to three workgroups per CU; unpinned the int32 store instantiation drifted to 174 VGPRs)
 #endif
@@ -2803,14 +2811,15 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
         if (mown) {
             // (round 5) the kept states' moments ride on this tile's digit planes while the
             // MFMAs run: wave w sums coordinates 16w..16w+15 of the chunk over the tile's 64
-            // rows, lane (4 coordinates: lane & 3) x (4 rows: lane >> 2), packed per row as
+            // rows, lane (4 coordinates: lane >> 4) x (4 rows: lane & 15), packed per row as
             // z^2 * 2^24 + (z + 32768) (64 rows: the low field < 2^22, the total < 2^63;
-            // rows past n hold z = 0 and add the bias only), then across the 16 lane groups
-            const int kk = 16 * wave + 4 * (lane & 3);
+            // rows past n hold z = 0 and add the bias only), then over the 16 lanes of a
+            // DPP row (row_ror 8, 4, 2, 1: VALU moves, no LDS round trip)
+            const int kk = 16 * wave + 4 * (lane >> 4);
             unsigned long long ps[4] = {0ull, 0ull, 0ull, 0ull};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int row = 4 * (lane >> 2) + i;
+                const int row = 4 * (lane & 15) + i;
                 const unsigned int lo4 = *(const unsigned int*)&Zs0[row * P + kk];
                 const unsigned int hi4 = *(const unsigned int*)&Zs1[row * P + kk];
 #pragma unroll
@@ -2820,10 +2829,13 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
                 }
             }
 #pragma unroll
-            for (int o = 4; o < 64; o <<= 1)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) ps[j] += __shfl_xor(ps[j], o);
-            if (lane < 4) {
+            for (int j = 0; j < 4; ++j) {
+                ps[j] += dpp_row_ror_u64<0x128>(ps[j]);  // row_ror:8
+                ps[j] += dpp_row_ror_u64<0x124>(ps[j]);  // row_ror:4
+                ps[j] += dpp_row_ror_u64<0x122>(ps[j]);  // row_ror:2
+                ps[j] += dpp_row_ror_u64<0x121>(ps[j]);  // row_ror:1
+            }
+            if ((lane & 15) == 0) {
                 unsigned long long* mp = MP + (size_t)ty * mp_ld + c0 + kk;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) mp[j] = ps[j];
@@ -3444,7 +3456,7 @@ hipError_t bz_moments_reduce(const unsigned long long* MP, const unsigned int* M
                              int d, unsigned long long* mom, const unsigned int* flags, hipStream_t st,
                              const unsigned int* abort) {
     if (ntiles <= 0) return hipSuccess;
-    const int64_t per = 128;  // tiles per workgroup
+    const int64_t per = 32;  // tiles per workgroup
     const dim3 grid((unsigned)((d + 255) / 256), (unsigned)((ntiles + per - 1) / per));
     hipLaunchKernelGGL(bz_moments_reduce_kernel, grid, dim3(256), 0, st, MP, MPL, ntiles, mp_ld, d, per, mom,
                        flags, abort);
