@@ -374,6 +374,10 @@ def main():
             "what": "executed fp64 flops (VALU FMA x2 + ADD/MUL + fp64 MFMA) per launch / the profiled launch's "
                     "rocprof duration; FP64 pipe peak",
             "kernel_ms_rocprof": round(p_s * 1e3, 3),
+            "profile_env": cnt.get("profile_env", {}),
+            "profile_note": "counters and rocprof duration of the same bench command with isolated launches "
+                            "(LGS_NO_PIPE=1: under the profiler the pipelined launches overlap differently); "
+                            "kernel_ms_avg is this run's HIP-event time of the pipelined launches",
             "traffic": int(cnt["hbm_bytes"]),
             "traffic_note": "FETCH_SIZE x2 + WRITE_SIZE per launch (gfx950 correction), profile of this command",
             "hbm": {"achieved_GBs": round(cnt["hbm_bytes"] / p_s / 1e9, 1),

@@ -10,6 +10,13 @@ export TMPDIR=/tmp
 TAG=${1:-r02}
 CFG=${2:-C3_ntru512}
 ARGS="--steps 3 --warmup 1 --no-cpu --wl-steps 0 --config $CFG"
+# Isolated launches (round 5): the bench pipelines each block's Klein launch beside the
+# previous block's B z; under rocprofv3 that overlap changes (the profiled bench ran at
+# 93.8 instead of 105 M samples/s, its Klein launches stretched to 10.0 ms by both
+# clocks, profiles/r05x_*), so the counters and the kernel's duration come from the
+# same command with LGS_NO_PIPE=1, where each launch has the chip to itself
+# (PROF_NO_PIPE=0: profile the pipelined command)
+export LGS_NO_PIPE=${PROF_NO_PIPE:-1}
 O=gpurun_out/prof_$TAG
 mkdir -p $O profiles
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py $ARGS > $O/bench_trace.log 2>&1 || { tail -20 $O/bench_trace.log; exit 1; }

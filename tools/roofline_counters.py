@@ -83,5 +83,9 @@ if len(sys.argv) > 7 and os.path.exists(sys.argv[7]):  # code-object resources o
                                                                "group_segment_fixed_size", "waves_per_simd")}
                           for k in co["kernels"] if "klein_mfma_kernel" in k["name"] or "bz_i8" in k["name"]}
     res["code_object_build_id"] = co.get("build_id")
+# the profiled command's library switches (tools/gpu_roofline.sh profiles isolated
+# launches: LGS_NO_PIPE=1, see there)
+res["profile_env"] = {k: os.environ[k] for k in ("LGS_NO_PIPE", "LGS_NO_LOOKAHEAD", "LGS_NO_BZ_MOMENTS")
+                      if k in os.environ}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: v for k, v in res.items() if k != "counters_per_launch"}))
