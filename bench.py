@@ -3,8 +3,8 @@
 Workload (BASELINE.json configs[2], the config the metric is quoted on):
 NTRU n=512, q=12289 basis [[qI,0],[H,I]] (d = 1024, Philox-generated h),
 sigma = 165.7, IMHK with 2^14 chains per GPU.  One bench step = one
-``lgs_imhk`` call advancing every chain by --imhk-steps steps: 2^14 x 64 =
-2^20 Klein proposals (back-substitution + SampleZ + importance weight), the
+``lgs_imhk`` call advancing every chain by --imhk-steps steps: 2^14 x 256 =
+2^22 Klein proposals in one block (back-substitution + SampleZ + importance weight), the
 Metropolis scan, exact integer moments, and the lattice points v = B z of every
 kept state (thin = 1), all resident in HBM; then the lag-L autocovariance sums
 of two scalar functionals of the first 1024 chains' kept states (a coefficient and
@@ -72,7 +72,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3_ntru512", choices=sorted(WORKLOADS))
     ap.add_argument("--chains", type=int, default=0, help="IMHK chains per GPU (default per config)")
-    ap.add_argument("--imhk-steps", type=int, default=64, help="IMHK steps per bench step (one lgs_imhk call)")
+    # (round 5: 256 -- one 2^22-proposal block per call at the library's default cap --
+    # 111 vs 105 M samples/s at 64, profiles/r05aa_*, r05ab_*)
+    ap.add_argument("--imhk-steps", type=int, default=256, help="IMHK steps per bench step (one lgs_imhk call)")
     ap.add_argument("--no-v", action="store_true", help="skip lattice points (coefficients only)")
     ap.add_argument("--exact-order", action="store_true")
     ap.add_argument("--cpu-samples", type=int, default=0,
@@ -180,7 +182,7 @@ def wang_ling_leg(args, ctx, D, _capi, lgs_oracle, R, cp, B, sigma, d, nc, T, se
                              gram_every=args.gram_every)
     ctx.counter(_capi.LGS_COUNTER_ACCEPT_RESOLVED, reset=True)
     ctx.counter(_capi.LGS_COUNTER_WL_MISMATCH, reset=True)
-    shard.step(T)  # warm-up block (initial draws + 64 steps)
+    shard.step(T)  # warm-up block (initial draws + T steps)
     torch.cuda.synchronize()
     acc0 = shard.acc.clone()
     t0 = time.perf_counter()

@@ -1161,10 +1161,12 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     c->sigma = sigma;
     c->precision = precision;
     c->basis_flags = flags;
-    // proposals per launch: keep the coefficient store around <= 8 GiB (288 GB of HBM;
-    // d = 4096 still gets 2^18 lanes = 4096 waves, enough to fill the 256 CUs)
-    const int64_t cap = std::max<int64_t>(256, (int64_t)((size_t)8 << 30) / (8 * d));
-    if (!getenv("LGS_MAX_PROPOSALS")) c->max_props = std::min<int64_t>(std::max<int64_t>(cap, 256), 1 << 20);
+    // proposals per launch: the coefficient store up to 32 GiB (288 GB of HBM; a
+    // pipelined lgs_imhk holds two such sets) and 2^22 proposals (round 5: a 2^21-
+    // proposal block runs the C3 bench at 110 vs 105 M samples/s -- the launch's tail
+    // and the per-block work amortised, profiles/r05aa_bench_ab.log)
+    const int64_t cap = std::max<int64_t>(256, (int64_t)((size_t)32 << 30) / (8 * d));
+    if (!getenv("LGS_MAX_PROPOSALS")) c->max_props = std::min<int64_t>(std::max<int64_t>(cap, 256), 1 << 22);
     return LGS_OK;
 }
 
