@@ -48,6 +48,15 @@ constexpr int kSzcStride = 24;
 // [0, kSzUsed), then c', 1/R_ii, R_ii/sigma, 1/sigma_i^ref, lterm, and the 15
 // near-field coefficients R[i-1-m][i] of the coordinate's 16-row sub-panel.
 // Staged into LDS once per 32-row panel by klein_mfma_kernel.
+#ifdef LGS_REC_L2
+// (variant) the dispatch code and the weight constants before the near-field
+// coefficients: the step's decision then waits for the first 15 of the record's 22
+// 16-byte reads, and Rs[1..14] arrive while it runs
+constexpr int kRecCp = kSzUsed, kRecIrii = kSzUsed + 1, kRecDisp = kSzUsed + 2, kRecRos = kSzUsed + 3,
+              kRecIsr = kSzUsed + 4, kRecLterm = kSzUsed + 5, kRecCbC = kSzUsed + 6, kRecRs = kSzUsed + 7;
+constexpr int kRecScale = kRecRs + 15;
+constexpr int kRecSpec = kRecScale + 1;
+#else
 constexpr int kRecCp = kSzUsed, kRecIrii = kSzUsed + 1, kRecRos = kSzUsed + 2,
               kRecIsr = kSzUsed + 3, kRecLterm = kSzUsed + 4, kRecRs = kSzUsed + 5;
 // SampleZ dispatch code of the coordinate (host): 0.0 = small kind with one dominant
@@ -57,14 +66,17 @@ constexpr int kRecDisp = kRecRs + 15;
 // int8-digit far field (klein_mfma_kernel OZ): row scale 2^E_i of the
 // coordinate's row over its panel's far columns
 constexpr int kRecScale = kRecRs + 16;
+#endif
 // 1.0 when the coordinate's 16-row sub-panel is whole and all its coordinates are
 // of the small kind with one dominant window point possible (q[7] == 0): the
 // sub-panel is then decided speculatively in parallel (klein_mfma_kernel)
+#ifndef LGS_REC_L2
 constexpr int kRecSpec = kRecScale + 1;
 // Cb of the certificate for a mean whose far field used only the 3 most significant
 // R digits (reference mode, panels of two speculative sub-panels: klein_mfma_kernel)
 constexpr int kRecCbC = kRecScale + 2;
-constexpr int kRecStride = kRecRs + 20;  // 48: 384 bytes, 16-byte multiple
+#endif
+constexpr int kRecStride = 48;  // 384 bytes, 16-byte multiple
 static_assert(kRecCbC < kRecStride, "record layout");
 constexpr int kOzCoarse = 4;  // R digits of the far field in coarse panels
 // int8-digit far field layout: per 32-row panel pk >= 1 (K = 32 pk far columns,

@@ -158,7 +158,12 @@ __device__ __forceinline__ double decide_coord(const KleinArgs& a, int i, double
 // round 4: off by default -- without it, and with the Philox products as mul_lo /
 // mul_hi pairs, the kernel spills 49 instead of 63 VGPRs and runs C2 / C3 / C4 / C5
 // 4 / 2 / 3 / 3 % faster, outputs identical, profiles/r04ac_kbench_mulhi_noripre.log)
-constexpr int kRecHot = kRecRs + 16;  // through the 15 near-field coefficients (44 doubles)
+#ifdef LGS_REC_L2
+constexpr int kRecHot = 46;  // (with the coarse panels' Cb, read in the batch instead of on its own)
+#else
+constexpr int kRecHot = 44;  // through the 15 near-field coefficients and the dispatch code
+#endif
+static_assert(kRecDisp < kRecHot && kRecRs + 15 <= kRecHot && kRecLterm < kRecHot, "hot record fields");
 struct RecRegs {
     double v[kRecHot];
 #ifdef LGS_CAP_RI_PRE
@@ -174,6 +179,24 @@ __device__ __forceinline__ RecRegs load_rec(lds_cdptr rec, MID mid = MID{}) {
     typedef double d2v __attribute__((ext_vector_type(2)));
     using lds_d2p = const __attribute__((address_space(3))) d2v*;
     RecRegs r;
+#ifdef LGS_REC_SPLIT
+    // (variant) the decision's fields and the dispatch code first (pairs 0..13, then
+    // pair 21: Rs[14] and the code), the near-field coefficients Rs[0..13] last and
+    // not pinned: LDS reads return in order, so the decision waits for 15 of the 22
+    // reads and the coefficients arrive while it runs
+#pragma unroll
+    for (int i = 0; i < kRecHot / 2; ++i) {
+        const int k = i < 14 ? i : (i == 14 ? kRecHot / 2 - 1 : i - 1);
+        const d2v t = ((lds_d2p)rec)[k];
+        r.v[2 * k] = t[0];
+        r.v[2 * k + 1] = t[1];
+    }
+    mid();
+#pragma unroll
+    for (int k = 0; k < kRecHot; ++k)
+        if (k < kRecRs || k >= kRecRs + 14) asm volatile("" : "+v"(r.v[k]));
+    return r;
+#endif
 #pragma unroll
     for (int k = 0; k < kRecHot / 2; ++k) {
         const d2v t = ((lds_d2p)rec)[k];
@@ -188,10 +211,19 @@ __device__ __forceinline__ RecRegs load_rec(lds_cdptr rec, MID mid = MID{}) {
     // pinned here: left alone, the compiler sinks each read into the branch that
     // uses it (three round trips after the kind / window branches)
 #pragma unroll
-    for (int k = 0; k < kRecHot; ++k) asm volatile("" : "+v"(r.v[k]));
+    for (int k = 0; k < kRecHot; ++k)
+#ifdef LGS_REC_L2  // (Rs[1..14] not pinned: the first use waits for them)
+        if (k <= kRecRs)
+#endif
+            asm volatile("" : "+v"(r.v[k]));
 #endif
     return r;
 }
+#ifdef LGS_REC_L2
+#define REC_CBC rr[kRecCbC]
+#else
+#define REC_CBC rec[kRecCbC]
+#endif
 struct RecView {  // q[k] of the SampleZ functions, served from the registers
     const RecRegs& r;
     __device__ __forceinline__ double operator[](int k) const { return r.v[k]; }
@@ -1535,12 +1567,12 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                                                                  cert_dmu(rr[kSzCa], rr[kSzCb], a.z1cap, mu), un, eb, tb)
                                          : decide_coord_rec<WL, true, LIBM>(
                                                a, i, mu, rec, rr, rs, lw, flags, etab_s,
-                                               cert_dmu(rr[kSzCa], coarse ? rec[kRecCbC] : rr[kSzCb], a.z1cap, mu), un,
+                                               cert_dmu(rr[kSzCa], coarse ? REC_CBC : rr[kSzCb], a.z1cap, mu), un,
                                                eb, tb);
 #else
                     const double zi = decide_coord_rec<WL, true, LIBM>(
                         a, i, mu, rec, rr, rs, lw, flags, etab_s,
-                        cert_dmu(rr[kSzCa], coarse ? rec[kRecCbC] : rr[kSzCb], a.z1cap, mu), un, eb, tb);
+                        cert_dmu(rr[kSzCa], coarse ? REC_CBC : rr[kSzCb], a.z1cap, mu), un, eb, tb);
 #endif
 #ifdef LGS_TAIL3
                     if (__builtin_amdgcn_ballot_w64(un) != 0) flm |= un ? (1 << s) : 0;  // (rare)
