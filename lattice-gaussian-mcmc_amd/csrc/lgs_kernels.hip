@@ -179,24 +179,6 @@ __device__ __forceinline__ RecRegs load_rec(lds_cdptr rec, MID mid = MID{}) {
     typedef double d2v __attribute__((ext_vector_type(2)));
     using lds_d2p = const __attribute__((address_space(3))) d2v*;
     RecRegs r;
-#ifdef LGS_REC_SPLIT
-    // (variant) the decision's fields and the dispatch code first (pairs 0..13, then
-    // pair 21: Rs[14] and the code), the near-field coefficients Rs[0..13] last and
-    // not pinned: LDS reads return in order, so the decision waits for 15 of the 22
-    // reads and the coefficients arrive while it runs
-#pragma unroll
-    for (int i = 0; i < kRecHot / 2; ++i) {
-        const int k = i < 14 ? i : (i == 14 ? kRecHot / 2 - 1 : i - 1);
-        const d2v t = ((lds_d2p)rec)[k];
-        r.v[2 * k] = t[0];
-        r.v[2 * k + 1] = t[1];
-    }
-    mid();
-#pragma unroll
-    for (int k = 0; k < kRecHot; ++k)
-        if (k < kRecRs || k >= kRecRs + 14) asm volatile("" : "+v"(r.v[k]));
-    return r;
-#endif
 #pragma unroll
     for (int k = 0; k < kRecHot / 2; ++k) {
         const d2v t = ((lds_d2p)rec)[k];
