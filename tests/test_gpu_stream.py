@@ -456,3 +456,58 @@ def test_pipelined_blocks_equal_synchronised_calls(capi, mode, plan):
     # moments: sum over every kept state of z and z^2 (exact integers)
     assert np.array_equal(a["mom"][:B.shape[0]], zrec.astype(np.int64).sum(0))
     assert np.array_equal(a["mom"][B.shape[0]:], (zrec.astype(np.int64) ** 2).sum(0))
+
+
+def test_lookahead_discarded_on_new_basis_and_changed_call(capi):
+    """A pipelined call leaves the next call's first Klein launch enqueued; lgs_set_basis
+    (another lattice) and a call with other arguments (another seed) must discard it:
+    the later calls equal the same calls on a fresh context."""
+    import torch
+    from conftest import golden_R, load_golden
+    ga, gb = load_golden("klein_qary128.npz"), load_golden("klein_ntru128.npz")
+    Ra, cpa, Ba = golden_R(ga)
+    Rb, cpb, Bb = golden_R(gb)
+    assert Ra.shape == Rb.shape
+    d, nc, steps = Ra.shape[0], 256, 8
+    dev = "cuda:0"
+
+    def state():
+        return dict(z=torch.zeros((d, nc), dtype=torch.int32, device=dev),
+                    lw=torch.zeros(nc, dtype=torch.float64, device=dev),
+                    init=torch.zeros(nc, dtype=torch.int32, device=dev),
+                    acc=torch.zeros(nc, dtype=torch.int64, device=dev),
+                    mom=torch.zeros(2 * d, dtype=torch.int64, device=dev))
+
+    def call(ctx, st, seed, first, B):
+        v = torch.zeros((nc, steps, d), dtype=torch.float64, device=dev)
+        ctx.imhk(seed, 0, nc, first, steps, 1, st["z"], st["lw"], st["init"], st["acc"], v_samples=v,
+                 moments=st["mom"], flags=capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR)
+        return v
+
+    s = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize()
+    ctx = capi.Context(0)
+    ctx.set_stream(s.cuda_stream)
+    with torch.cuda.stream(s):
+        ctx.set_basis(Ra, cpa, Ba, float(ga["sigma"]))
+        call(ctx, state(), 3, 1, Ba)  # leaves a look-ahead for (seed 3, step 9) on basis a
+        ctx.set_basis(Rb, cpb, Bb, float(gb["sigma"]))
+        st1 = state()
+        v1 = call(ctx, st1, 3, 9, Bb)  # the look-ahead's arguments, but another basis
+        v2 = call(ctx, st1, 4, 17, Bb)  # another seed than this call's look-ahead
+    torch.cuda.synchronize()
+    got = [v1.cpu().numpy(), v2.cpu().numpy(), st1["z"].cpu().numpy(), st1["mom"].cpu().numpy()]
+    ctx.close()
+    ref = capi.Context(0)  # fresh, on its own stream (host-checked calls)
+    ref.set_basis(Rb, cpb, Bb, float(gb["sigma"]))
+    st2 = state()
+    w1 = call(ref, st2, 3, 9, Bb)
+    w2 = call(ref, st2, 4, 17, Bb)
+    torch.cuda.synchronize()
+    want = [w1.cpu().numpy(), w2.cpu().numpy(), st2["z"].cpu().numpy(), st2["mom"].cpu().numpy()]
+    ref.close()
+    for g_, w_ in zip(got, want):
+        assert np.array_equal(g_, w_)
+    # v = B z for the fresh basis (not the look-ahead's)
+    zrec = np.rint(np.linalg.solve(Bb.astype(np.float64), got[0].reshape(-1, d).T)).T
+    assert np.array_equal(Bb.astype(np.float64) @ zrec.T, got[0].reshape(-1, d).T)
