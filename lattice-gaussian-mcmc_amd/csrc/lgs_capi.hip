@@ -611,7 +611,7 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
     if (diag_bz & 2) sel = nullptr;
     double* VNP = nullptr;
     if (VN) {
-        const int rc = c->VNP.reserve((size_t)2 * ((c->d + 127) / 128) * vn_n * 8);
+        const int rc = c->VNP.reserve((size_t)2 * ((c->d + lgs::kBzBN - 1) / lgs::kBzBN) * vn_n * 8);
         if (rc) return rc;
         VNP = c->VNP.as<double>();
     }

@@ -77,6 +77,12 @@ constexpr int kRecSpec = kRecScale + 1;
 constexpr int kRecCbC = kRecScale + 2;
 #endif
 constexpr int kRecStride = 48;  // 384 bytes, 16-byte multiple
+#ifndef LGS_BZ_BN
+#define LGS_BZ_BN 128
+#endif
+// B z (bz_i8_kernel): coordinates per workgroup tile (128, or 64: half the
+// accumulators per wave, twice the workgroups)
+constexpr int kBzBN = LGS_BZ_BN;
 static_assert(kRecCbC < kRecStride, "record layout");
 constexpr int kOzCoarse = 4;  // R digits of the far field in coarse panels
 // int8-digit far field layout: per 32-row panel pk >= 1 (K = 32 pk far columns,

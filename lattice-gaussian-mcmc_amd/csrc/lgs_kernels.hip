@@ -2641,7 +2641,8 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
                                                     unsigned int* __restrict__ MPL) {
     if (aborted(abort)) return;  // (whole grid) the selections were not written
     constexpr int TA = LGS_BZ_TA;  // 32-sample MFMA tiles per wave
-    constexpr int BM = 64 * TA, BN = 128, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
+    constexpr int BM = 64 * TA, BN = kBzBN, KC = 64, P = 80;  // P: LDS row pitch (bytes), conflict-free
+    constexpr int TN = BN / 64;  // 32-coordinate MFMA tiles per wave (waves 2 x 2)
     constexpr int KPT = KC * BM / 256;  // coefficients per thread per chunk
     __shared__ __attribute__((aligned(16))) int8_t Zs1[BM * P], Zs0[BM * P], Bs1[BN * P], Bs0[BN * P];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2662,11 +2663,11 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
     ZT zmax = 0, zmin = 0;  // range of the coefficients read (exactness check)
     for (int tx = txg * LGS_BZ_TXPER; tx < ntx && tx < (txg + 1) * LGS_BZ_TXPER; ++tx) {
     const int r0 = tx * BN;
-    v16i_t p1[TA][2], p2[TA][2], p3[TA][2];
+    v16i_t p1[TA][TN], p2[TA][TN], p3[TA][TN];
 #pragma unroll
     for (int ta = 0; ta < TA; ++ta)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < TN; ++t) {
             p1[ta][t] = (v16i_t){};
             p2[ta][t] = (v16i_t){};
             p3[ta][t] = (v16i_t){};
@@ -2675,11 +2676,12 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
     const int64_t zs_ = s0 + zm;
     const int64_t zcol = zs_ < n ? (sel ? sel[zs_] : zs_) : 0;  // this thread's sample column
     // only the K chunks where this row tile of B has a non-zero digit (exact skip)
-    const int ci0 = koff[tx];
+    // (the block-sparsity lists are per 128-row tile of B)
+    const int ci0 = koff[tx * BN / 128];
 #ifdef LGS_DIAG_BZ_NOMFMA  // diagnostic builds only: epilogue cost probe
     const int ci1 = ci0;
 #else
-    const int ci1 = koff[tx + 1];
+    const int ci1 = koff[tx * BN / 128 + 1];
 #endif
     // Chunks where every sample of the tile has z = 0 on all 64 coordinates contribute
     // exactly nothing: skipped.  The Klein launch that wrote the history flags each
@@ -2759,7 +2761,7 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
         // (bit 16 of a chunk entry: this row tile owns the chunk's moments, MP)
         const int kraw = kchunk[ci];
         const int cix = kraw & 0xffff;
-        const bool mown = MP != nullptr && (kraw >> 16) != 0 && KPT == 16;
+        const bool mown = MP != nullptr && (kraw >> 16) != 0 && KPT == 16 && (BN == 128 || (tx & 1) == 0);
         if ((use_clive && !(((ngw == 1 ? live1 : livew4[wave][cix >> 5]) >> (cix & 31)) & 1u)) ||
             (use_znz && !((livew[(ci - ci0) >> 5] >> ((ci - ci0) & 31)) & 1u))) {  // (uniform)
             continue;  // (an all-zero chunk's moment partials stay 0: MP is cleared per launch)
@@ -2814,7 +2816,7 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
             }
         }
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {  // B digit planes [coord][k], 16 B per thread per plane
+        for (int e = 0; e < BN / 64; ++e) {  // B digit planes [coord][k], 16 B per thread per plane
             const int idx = tid + 256 * e;
             const int row = idx >> 2, part = idx & 3;
             const size_t g = (size_t)(r0 + row) * dc + c0 + part * 16;
@@ -2866,8 +2868,8 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
                 a0[ta] = *(const v4i_t*)&Zs0[arow * P + kb];
             }
 #pragma unroll
-            for (int tn = 0; tn < 2; ++tn) {
-                const int col = wn * 64 + tn * 32 + (lane & 31);
+            for (int tn = 0; tn < TN; ++tn) {
+                const int col = wn * (BN / 2) + tn * 32 + (lane & 31);
                 const v4i_t b1 = *(const v4i_t*)&Bs1[col * P + kb];
                 const v4i_t b0 = *(const v4i_t*)&Bs0[col * P + kb];
 #pragma unroll
@@ -2905,8 +2907,8 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
         for (int reg = 0; reg < 16; ++reg) {
             vs[reg] = 0.0;
 #pragma unroll
-            for (int tn = 0; tn < 2; ++tn)
-                if (r0 + wn * 64 + tn * 32 + (lane & 31) < d) {
+            for (int tn = 0; tn < TN; ++tn)
+                if (r0 + wn * (BN / 2) + tn * 32 + (lane & 31) < d) {
                     const double v = fma((double)p1[ta][tn][reg], 65536.0, (double)p2[ta][tn][reg] * 256.0) +
                                      (double)p3[ta][tn][reg];
                     vs[reg] = fma(v, v, vs[reg]);
@@ -2935,7 +2937,7 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
     const int nrow = (int)min<int64_t>(n - qb, 32);  // valid rows of this tile
     if (rb >= 32) {
         const int wrap_row = (int)min<int64_t>(rb - kb0, 32);  // first row past the boundary
-        double* const vbase = V + (size_t)(cb * rstride + roff + kb0) * ldv + r0 + wn * 64 + (lane & 31);
+        double* const vbase = V + (size_t)(cb * rstride + roff + kb0) * ldv + r0 + wn * (BN / 2) + (lane & 31);
         const int64_t jump = (rstride - rb) * ldv;
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
@@ -2943,8 +2945,8 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
             if (row >= nrow) continue;
             double* vrow = vbase + (size_t)row * ldv + (row >= wrap_row ? jump : 0);
 #pragma unroll
-            for (int tn = 0; tn < 2; ++tn) {
-                if (r0 + wn * 64 + tn * 32 + (lane & 31) < d) {
+            for (int tn = 0; tn < TN; ++tn) {
+                if (r0 + wn * (BN / 2) + tn * 32 + (lane & 31) < d) {
                     const double v = fma((double)p1[ta][tn][reg], 65536.0, (double)p2[ta][tn][reg] * 256.0) +
                                      (double)p3[ta][tn][reg];
 #ifdef LGS_DIAG_BZ_NOSTORE  // diagnostic builds only: store cost probe
@@ -2965,8 +2967,8 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
             const int64_t orow = (cb + wrap) * rstride + roff + (kk - wrap * urb);
             double* vrow = V + (size_t)orow * ldv;
 #pragma unroll
-            for (int tn = 0; tn < 2; ++tn) {
-                const int r = r0 + wn * 64 + tn * 32 + (lane & 31);
+            for (int tn = 0; tn < TN; ++tn) {
+                const int r = r0 + wn * (BN / 2) + tn * 32 + (lane & 31);
                 if (r < d) {
                     const double v = fma((double)p1[ta][tn][reg], 65536.0, (double)p2[ta][tn][reg] * 256.0) +
                                      (double)p3[ta][tn][reg];
@@ -3334,7 +3336,7 @@ hipError_t coord_gather(const void* Z, int zb, int64_t ldz, const int64_t* sel, 
 hipError_t vnorm2_reduce(const double* VNP, int d, int64_t n, int64_t rb, int64_t rstride, int64_t roff,
                          double* VN, hipStream_t st, const unsigned int* abort) {
     if (n <= 0) return hipSuccess;
-    const int nparts = 2 * ((d + 127) / 128);
+    const int nparts = 2 * ((d + kBzBN - 1) / kBzBN);
     hipLaunchKernelGGL(vnorm2_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, VNP, nparts, n, rb,
                        rstride, roff, VN, abort);
     return hipGetLastError();
@@ -3459,7 +3461,7 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
 #ifdef LGS_DIAG_BZ_NO_SEL  // diagnostic builds only (identity selections, e.g. acceptance 1): gather cost
     sel = nullptr;
 #endif
-    const int tx = ((d + 127) / 128 + LGS_BZ_TXPER - 1) / LGS_BZ_TXPER;  // coordinate-tile groups
+    const int tx = ((d + kBzBN - 1) / kBzBN + LGS_BZ_TXPER - 1) / LGS_BZ_TXPER;  // coordinate-tile groups
     const int64_t ty = (n + 64 * LGS_BZ_TA - 1) / (64 * LGS_BZ_TA);
     const dim3 grid((unsigned)(tx * ((ty + 7) / 8) * 8));  // whole rounds of 8 XCDs (extra tiles exit)
     LGS_ZT(zb, ZT, hipLaunchKernelGGL(bz_i8_kernel<ZT>, grid, dim3(256), 0, st, (const ZT*)Z, ldz, sel, kchunk, koff, Bd1, Bd0, dc, d, n, V, ldv, rb, rstride, roff, flags, tx, ty, h16, h16_lanes, hcols, abort, znz, clive, clive_ld, VNP, vn_n, MP, mp_ld, MPL));
