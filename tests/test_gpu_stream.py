@@ -372,7 +372,8 @@ def test_early_check_equals_synchronised_call(capi, zmax):
             np.testing.assert_allclose(got, w, rtol=1e-12, atol=0)
 
 
-def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, blocks: int = 3, plan=None):
+def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, blocks: int = 3, plan=None,
+                thin: int = 1, z64: bool = False):
     """Several lgs_imhk_ex calls of several blocks each (LGS_MAX_PROPOSALS: T = 4 steps
     per block), chain state, accept counts, moments, lattice points, functionals and
     lag sums carried across them -- on a caller's stream the blocks are pipelined
@@ -395,11 +396,13 @@ def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, 
     ctx.set_basis(R, cp, B, float(g["sigma"]))
     dev = "cuda:0"
     plan = plan or [T * blocks] * calls  # steps per call (a changed count discards the look-ahead launch)
-    z = torch.zeros((d, nc), dtype=torch.int32, device=dev)
+    z = torch.zeros((d, nc), dtype=torch.int64 if z64 else torch.int32, device=dev)
     lw = torch.zeros(nc, dtype=torch.float64, device=dev)
     init = torch.zeros(nc, dtype=torch.int32, device=dev)
     acc = torch.zeros(nc, dtype=torch.int64, device=dev)
     mom = torch.zeros(2 * d, dtype=torch.int64, device=dev)
+    if z64:
+        flags_extra |= capi.LGS_Z64
     L = 5
     zr = torch.zeros((nc, L), dtype=torch.int64, device=dev)
     zsum = torch.zeros(L + 2, dtype=torch.int64, device=dev)
@@ -413,10 +416,11 @@ def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, 
     with torch.cuda.stream(s):
         first = 1
         for steps in plan:
-            vs = torch.zeros((nc, steps, d), dtype=torch.float64, device=dev)
-            vn2 = torch.zeros((nc, steps), dtype=torch.float64, device=dev)
-            zk = torch.zeros((nc, steps), dtype=torch.int64, device=dev)
-            ctx.imhk(11, 0, nc, first, steps, 1, z, lw, init, acc, v_samples=vs, moments=mom,
+            kept = steps // thin
+            vs = torch.zeros((nc, kept, d), dtype=torch.float64, device=dev)
+            vn2 = torch.zeros((nc, kept), dtype=torch.float64, device=dev)
+            zk = torch.zeros((nc, kept), dtype=torch.int64, device=dev)
+            ctx.imhk(11, 0, nc, first, steps, thin, z, lw, init, acc, v_samples=vs, moments=mom,
                      vnorm2_samples=vn2, zk_samples=zk, zk_index=5,
                      flags=capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR | flags_extra,
                      lag=(L, zr, zsum, vr, vsum, 1e-6))
@@ -434,8 +438,10 @@ def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, 
     return B, out
 
 
-@pytest.mark.parametrize("mode,plan", [("reference", None), ("wang_ling_exact", None), ("reference", [12, 4, 4, 8])])
-def test_pipelined_blocks_equal_synchronised_calls(capi, mode, plan):
+@pytest.mark.parametrize("mode,plan,thin,z64", [("reference", None, 1, False), ("wang_ling_exact", None, 1, False),
+                                               ("reference", [12, 4, 4, 8], 1, False), ("reference", None, 2, False),
+                                               ("reference", None, 1, True)])
+def test_pipelined_blocks_equal_synchronised_calls(capi, mode, plan, thin, z64):
     """Pipelined blocks (caller's stream) give every output of the host-checked calls
     on the library's own stream, bit for bit, over 3 calls x 3 blocks (each call's
     first block from the previous call's look-ahead launch), or calls of 3, 1, 1 and 2
@@ -443,11 +449,11 @@ def test_pipelined_blocks_equal_synchronised_calls(capi, mode, plan):
     one); v is B z of the kept states (z_k recovered from v through the basis' inverse
     is checked against zk)."""
     fx = 0 if mode == "reference" else capi.LGS_WANG_LING | capi.LGS_EXACT_ORDER
-    B, a = _imhk_calls(capi, True, fx, plan=plan)
-    _, b = _imhk_calls(capi, False, fx, plan=plan)
+    B, a = _imhk_calls(capi, True, fx, plan=plan, thin=thin, z64=z64)
+    _, b = _imhk_calls(capi, False, fx, plan=plan, thin=thin, z64=z64)
     for k in a:
         assert np.array_equal(a[k], b[k]), k
-    steps = a["v"].shape[1]
+    steps = a["v"].shape[1] * thin  # (thin 2: the moments and v count the kept states only)
     assert a["acc"].sum() > 0 and (mode == "reference") == bool((a["acc"] == steps).all())
     # v = B z: z = B^-1 v is integral and its coordinate 5 is the zk series
     zrec = np.rint(np.linalg.solve(B.astype(np.float64), a["v"].reshape(-1, B.shape[0]).T)).T
