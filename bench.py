@@ -398,6 +398,9 @@ def main():
     if g_n:
         gemm = {"kernel": "bz_gemm_kernel" if os.environ.get("LGS_BZ_FP64") == "1" else "bz_i8_kernel",
                 "ms_per_step": round(g_ms / args.steps, 3)}
+        if os.environ.get("LGS_NO_PIPE") != "1":
+            gemm["note"] = ("HIP-event span on the work stream, beside the next block's Klein launch (pipelined "
+                            "blocks): it stretches over that launch; LGS_NO_PIPE=1 times it alone")
 
     # ---- Wang-Ling leg (after the headline's timed region; not part of `value`):
     # the one IMHK mode whose acceptance is not identically 1 (imhk.py:102-124 gives a
