@@ -947,6 +947,14 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
     for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) t0v[g][reg] = 0.0;
+#ifdef LGS_XP_ALIAS
+    // the upper row tile too: F shares its LDS with the slab, which later passes still use
+    double t1v[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) t1v[g][reg] = 0.0;
+#endif
     auto slab_load = [&](int ch, v4i32_t (&pf)[4]) {
         const v4i32_t* src = rsrc + (size_t)ch * SLAB;
 #pragma unroll
@@ -1059,13 +1067,26 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
                     for (int c = NC - 2; c >= 0; --c) sv = fma(sv, 0.00390625, (double)cc[q][t][c][reg]);
                     const double fv = sv * rec[row * kRecStride + kRecScale];
                     if (t == 1) {
+#ifdef LGS_XP_ALIAS
+#pragma unroll
+                        for (int gg = 0; gg < 4; ++gg) t1v[gg][reg] = g == gg ? fv : t1v[gg][reg];
+#else
                         F[(4 * h + reg) * LDF + 16 * g + n] = fv;
+#endif
                     } else {
 #pragma unroll
                         for (int gg = 0; gg < 4; ++gg) t0v[gg][reg] = g == gg ? fv : t0v[gg][reg];
                     }
                 }
     }
+#ifdef LGS_XP_ALIAS
+    // every pass's chunk loop ended with a block barrier after its last slab reads (and
+    // a block without live chunks never touched the slab): F is free for every wave
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) F[(4 * h + reg) * LDF + 16 * g + n] = t1v[g][reg];
+#endif
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -1106,11 +1127,20 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                                                             ZT* __restrict__ Z) {
     if (a.gate && *a.gate == 0u) return;  // whole grid: nothing to draw
     constexpr int NT = PB / 16, LDF = 65;  // LDS tile pitch (doubles): conflict-free row reads
+#ifdef LGS_XP_ALIAS  // (experiment: the far-field tiles share the R-digit slab's LDS)
+    __shared__ __attribute__((aligned(16))) double Fl_raw[4 * 16 * LDF];
+    double (*Fl)[16 * LDF] = (double (*)[16 * LDF])Fl_raw;
+#else
     __shared__ double Fl[4][16 * LDF];
+#endif
     // OZ: the erf table stays in global memory (L1-resident lookups measured as fast
     // as LDS) to leave LDS for the block-shared R-digit slab of the far field
     __shared__ double tab_lds[OZ ? 2 : 2 * (kErfTabLast + 1)];
+#ifdef LGS_XP_ALIAS
+    int8_t* ash = (int8_t*)Fl_raw;
+#else
     __shared__ __attribute__((aligned(16))) int8_t ash[OZ ? 2 * 2 * kOzDigits * 1024 : 16];  // 2 x 14 KB
+#endif
 #ifdef LGS_COEF_ON  // Taylor-coefficient table: measured 2% slower (load latency)
     using ETP = std::conditional_t<OZ, CoefTab, lds_cdptr>;
     ETP etab_s;
