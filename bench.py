@@ -257,7 +257,10 @@ def main():
     cp = np.zeros(d)
     binv_k = np.linalg.inv(B)[d - 1]  # z_{d-1} = row d-1 of B^-1 times v (rounded: v, z integral)
 
-    ctx = _capi.Context(local)
+    # LGS_NO_PIPE=1 (read here, passed as lgs_create_ex's LGS_CTX_NO_PIPELINE): isolated
+    # launches, for the rocprof roofline passes (tools/gpu_roofline.sh)
+    pipelined = os.environ.get("LGS_NO_PIPE") != "1"
+    ctx = _capi.Context(local, pipeline=pipelined)
     ctx.set_basis(R, cp, B, sigma)
     nc = args.chains or WORKLOADS[args.config]["chains"]
     T = args.imhk_steps
@@ -396,9 +399,8 @@ def main():
         f"chain (read once per 256-sample block from L2), so B_alg x rate is not an HBM quantity")
     gemm = None
     if g_n:
-        gemm = {"kernel": "bz_gemm_kernel" if os.environ.get("LGS_BZ_FP64") == "1" else "bz_i8_kernel",
-                "ms_per_step": round(g_ms / args.steps, 3)}
-        if os.environ.get("LGS_NO_PIPE") != "1":
+        gemm = {"kernel": "bz_i8_kernel", "ms_per_step": round(g_ms / args.steps, 3)}
+        if pipelined:
             gemm["note"] = ("HIP-event span on the work stream, beside the next block's Klein launch (pipelined "
                             "blocks): it stretches over that launch; LGS_NO_PIPE=1 times it alone")
 
@@ -483,7 +485,7 @@ def main():
         "gemm": gemm,
         "kernel_ms": {"klein": round(k_ms / max(k_n, 1), 3), "bz": round(g_ms / max(g_n, 1), 3),
                       "accept": round(a_ms / max(a_n, 1), 3), "moments": round(m_ms / max(m_n, 1), 3),
-                      "blocks_pipelined": os.environ.get("LGS_NO_PIPE") != "1",
+                      "blocks_pipelined": pipelined,
                       "note": "pipelined blocks: each lgs_imhk block's Klein launch runs on the library's Klein "
                               "stream beside the previous block's accept / moments / B z on the work stream, so "
                               "these launch times overlap (their sum exceeds ms_per_step) and each is stretched by "

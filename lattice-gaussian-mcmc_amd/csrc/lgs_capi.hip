@@ -39,6 +39,21 @@ int fail(int code, const char* fmt, ...) {
                         __FILE__, __LINE__);                                             \
     } while (0)
 
+// Test / experiment switches read from the environment exist only in builds with
+// -DLGS_TEST_HOOKS (liblgs_hip_hooks.so, the A/B variants of tools/build_variant.sh):
+// in the product library hook() is a constant nullptr and every such branch folds
+// away, so nothing in a user's environment changes what the library computes.  The
+// real options are lgs_create_ex's arguments.
+#ifdef LGS_TEST_HOOKS
+static const char* hook(const char* name) { return getenv(name); }
+#else
+static constexpr const char* hook(const char*) { return nullptr; }
+#endif
+static bool hook_is(const char* name, int v) {
+    const char* e = hook(name);
+    return e && atoi(e) == v;
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -61,6 +76,11 @@ struct DevBuf {
         bytes = need;
         return LGS_OK;
     }
+    void release() {  // (hipFree waits for the device's work on it)
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
     template <typename T>
     T* as() const {
         return (T*)p;
@@ -70,6 +90,7 @@ struct DevBuf {
 struct Timer {
     int kernel;
     hipEvent_t a, b;
+    bool spec = false;  // a look-ahead launch's: dropped if the launch is discarded
 };
 
 struct BzCall {  // an int8-digit B z launch, replayed in fp64 if a digit overflowed
@@ -148,6 +169,8 @@ struct lgs_ctx {
     DevBuf Z, LW, V, sel, fsel, cnt, ccnt, flags, stage_a, stage_b, stage_c, stage_d, stage_e,
         stage_f, stage_g, stage_h, stage_i, vs;
     int64_t max_props = 1 << 18;
+    bool max_props_user = false;  // lgs_create_ex's cap (else set per basis, lgs_set_basis)
+    bool no_pipe = false, no_look = false, no_qskip = false;  // lgs_create_ex ctx_flags
     int zint = 2;  // internal coefficient store width (bytes): 16-bit, sticky 32-bit on overflow; LGS_ZINT=4 forces 32-bit
     // timing
     bool timing = false;
@@ -272,7 +295,22 @@ struct SetSwap {
         if (store_in) swap_store();
         if (flags_in) swap_flags();
     }
-    ~SetSwap() { restore(); }
+    // The block is over, on its normal path or an error return (a finish() error such
+    // as LGS_ERR_OVERFLOW / LGS_ERR_NONFINITE leaves the block's accept, B z, moments and
+    // gathers enqueued on the caller's stream, still reading the set): the buffers go
+    // back, and the set's free event is recorded behind whatever the block enqueued, so
+    // the set's next Klein launch (kstream) waits for those readers in every case.
+    bool record = true;  // (the look-ahead launch: no reader of its own on the caller's stream)
+    void release() {
+        if (j < 0) return;
+        restore();
+        if (record) {
+            (void)hipEventRecord(c->bset[j].ev_free, c->stream);
+            c->bset[j].free_recorded = true;
+        }
+        j = -1;
+    }
+    ~SetSwap() { release(); }
 };
 
 // Drops a look-ahead Klein launch (lgs_ctx::Spec): waits for it and clears the flag
@@ -282,6 +320,17 @@ int spec_discard(lgs_ctx* c) {
     c->spec.valid = false;
     HIP_TRY(hipStreamSynchronize(c->kstream));
     HIP_TRY(hipMemset(c->bset[c->spec.j].flags.p, 0, 4 * lgs::kFlagWords));
+    // its launch timers do not count (the launch's work is thrown away)
+    size_t keep = 0;
+    for (auto& t : c->pending) {
+        if (t.spec) {
+            c->pool.push_back(t.a);
+            c->pool.push_back(t.b);
+        } else {
+            c->pending[keep++] = t;
+        }
+    }
+    c->pending.resize(keep);
     return LGS_OK;
 }
 
@@ -342,7 +391,7 @@ void fold_counters(lgs_ctx* c, const unsigned int* fw) {
 void fold_timers(lgs_ctx* c) {
     size_t keep = 0;
     for (auto& t : c->pending) {
-        if (hipEventQuery(t.b) != hipSuccess) {
+        if (t.spec || hipEventQuery(t.b) != hipSuccess) {  // (a look-ahead's: until used or discarded)
             c->pending[keep++] = t;
             continue;
         }
@@ -473,11 +522,24 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
     a.z1cap = c->z1cap;
     // test hook: scale the certificate's cap on sum |z_j| (a cap below the actual sums
     // forces every 32-row-panel sub-panel through the verification / replay path)
-    if (const char* s = getenv("LGS_TEST_Z1CAP_SCALE")) a.z1cap *= atof(s);
+    if (const char* s = hook("LGS_TEST_Z1CAP_SCALE")) a.z1cap *= atof(s);
     a.z1max = (unsigned long long*)c->flags.as<unsigned int>() + 1;
-    const bool no_qskip = getenv("LGS_NO_QSKIP") && atoi(getenv("LGS_NO_QSKIP")) == 1;  // A/B switch
+    const bool no_qskip = c->no_qskip || hook_is("LGS_NO_QSKIP", 1);  // (LGS_CTX_NO_QSKIP: A/B)
     a.qz2 = c->has_qz2 && !no_qskip ? c->QZ2.as<double>() : nullptr;
     return a;
+}
+
+// The int8-digit far field's per-launch buffers for n proposals (the sizes run_klein
+// reserves; pre-reserved by lgs_imhk so that an allocation failure halves its block).
+int reserve_oz(lgs_ctx* c, DevBuf& H16, DevBuf& ZNZ, DevBuf& CLIVE, int64_t n) {
+    if (!(c->panel == 32 && c->has_rd)) return LGS_OK;
+    const int shift = (int)((16 - c->d % 16) % 16);
+    const int64_t lanes = (n + 63) / 64 * 64;
+    const int64_t blocks = (c->d + shift) / 16 + 5;
+    int rc = H16.reserve((size_t)blocks * lanes * 32);
+    if (!rc) rc = ZNZ.reserve((size_t)blocks * lanes);
+    if (!rc && c->d % 16 == 0) rc = CLIVE.reserve((size_t)((c->d + 2047) / 2048 * (lanes / 64)) * 4);
+    return rc;
 }
 
 // Kernel choice: exact order on request; otherwise the MFMA kernel when the launch
@@ -487,7 +549,7 @@ lgs::KleinArgs base_args(lgs_ctx* c, uint64_t seed) {
 // field was used.
 int run_klein(lgs_ctx* c, lgs::KleinArgs& a, bool exact, bool wl, int zb, void* Z, bool& used_oz) {
     Scope s(c, a.gate ? 6 : 0);  // gated launches (lgs_imhk's initial draws) on their own timer
-    static const char* force = getenv("LGS_KERNEL");
+    static const char* force = hook("LGS_KERNEL");
     int kernel = lgs::kKernelValu;
     used_oz = false;
     c->hist.Z = nullptr;
@@ -593,7 +655,7 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
     if (vn_n < 0 || vn_n > n) vn_n = n;  // ||v||^2 of the leading vn_n rows only
     if (vn_n == 0) VN = nullptr;
     BzCall b{Z, zb, ldz, n, V, rb > 0 ? rb : n, rstride, roff, sel, VN, vn_n};
-    static const bool force64 = getenv("LGS_BZ_FP64") && atoi(getenv("LGS_BZ_FP64")) == 1;
+    static const bool force64 = hook_is("LGS_BZ_FP64", 1);
     if (!c->has_Bi8 || force64) {
         Scope s(c, 1);
         HIP_TRY(lgs::launch::bz(b.Z, b.zb, b.ldz, b.sel, c->BT.as<double>(), (int)c->d, b.n, b.V, c->d, b.rb,
@@ -606,7 +668,7 @@ int run_bz(lgs_ctx* c, const void* Z, int zb, int64_t ldz, int64_t n, double* V,
     const int8_t* lo = hi + (size_t)c->bd_rows * c->bd_cols;
     // timing probes only (wrong outputs): LGS_DIAG_BZ=1 drops the ||v||^2 rows, 2 the
     // selections (row q reads proposal q), 3 both
-    static const int diag_bz = getenv("LGS_DIAG_BZ") ? atoi(getenv("LGS_DIAG_BZ")) : 0;
+    static const int diag_bz = hook("LGS_DIAG_BZ") ? atoi(hook("LGS_DIAG_BZ")) : 0;
     if (diag_bz & 1) VN = nullptr;
     if (diag_bz & 2) sel = nullptr;
     double* VNP = nullptr;
@@ -648,6 +710,7 @@ int lookahead(lgs_ctx* c, int j, uint64_t seed, uint64_t first_chain, uint64_t s
     SetSwap sw;
     sw.c = c;
     sw.j = j;
+    sw.record = false;
     sw.swap_flags();
     sw.swap_store();
     const int64_t ldz = nc * tb + (carry ? nc : 0);
@@ -665,7 +728,9 @@ int lookahead(lgs_ctx* c, int j, uint64_t seed, uint64_t first_chain, uint64_t s
     c->stream = c->kstream;
     int zbs = zb;
     bool oz = false;
+    const size_t npend = c->pending.size();
     const int rc = run_klein_store(c, a, exact, wl, zbs, c->Z.p, true, &oz);
+    for (size_t k = npend; k < c->pending.size(); ++k) c->pending[k].spec = true;
     c->stream = cs;
     const auto h = c->hist;
     c->hist = hist;
@@ -704,8 +769,11 @@ int lgs_version(void) { return 100; }
 
 const char* lgs_last_error(void) { return g_err.c_str(); }
 
-int lgs_create(lgs_ctx** out, int device) {
+int lgs_create(lgs_ctx** out, int device) { return lgs_create_ex(out, device, 0, 0); }
+
+int lgs_create_ex(lgs_ctx** out, int device, int64_t max_proposals, uint32_t ctx_flags) {
     if (!out) return fail(LGS_ERR_INVALID, "null out pointer");
+    if (max_proposals < 0) return fail(LGS_ERR_INVALID, "max_proposals < 0");
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
     if (device < 0 || device >= n)
@@ -719,16 +787,32 @@ int lgs_create(lgs_ctx** out, int device) {
         return fail(LGS_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
     c->stream = c->own;
-    if (const char* p = getenv("LGS_PANEL")) c->panel = atoi(p) == 16 ? 16 : 32;
-    if (const char* z = getenv("LGS_ZINT")) c->zint = atoi(z) == 2 ? 2 : 4;
-    if (const char* m = getenv("LGS_MAX_PROPOSALS")) {
-        long long v = atoll(m);
-        if (v >= 64) c->max_props = v;
-    }
-    if (const char* m = getenv("LGS_SAMPLEZ_LIBM")) c->libm_samplez = atoi(m) != 0;
+    // options (include/lgs.h LGS_CTX_*); the hooks build also takes them from the
+    // environment for the A/B tools
+    c->panel = (ctx_flags & LGS_CTX_PANEL16) ? 16 : 32;
+    c->zint = (ctx_flags & LGS_CTX_STORE32) ? 4 : 2;
+    c->libm_samplez = (ctx_flags & LGS_CTX_SAMPLEZ_LIBM) != 0;
     // far field of the 32-row-panel kernel: the exact int8-digit product (default)
-    // or fp64 MFMA (LGS_FAR=fp64)
-    if (const char* m = getenv("LGS_FAR")) c->oz_off = strcmp(m, "fp64") == 0;
+    // or fp64 MFMA (LGS_CTX_FAR_FP64)
+    c->oz_off = (ctx_flags & LGS_CTX_FAR_FP64) != 0;
+    c->no_pipe = (ctx_flags & LGS_CTX_NO_PIPELINE) != 0;
+    c->no_look = (ctx_flags & LGS_CTX_NO_LOOKAHEAD) != 0;
+    c->no_qskip = (ctx_flags & LGS_CTX_NO_QSKIP) != 0;
+    if (max_proposals > 0) {
+        c->max_props = std::max<int64_t>(64, max_proposals);
+        c->max_props_user = true;
+    }
+    if (const char* p = hook("LGS_PANEL")) c->panel = atoi(p) == 16 ? 16 : 32;
+    if (const char* z = hook("LGS_ZINT")) c->zint = atoi(z) == 2 ? 2 : 4;
+    if (const char* m = hook("LGS_MAX_PROPOSALS")) {
+        long long v = atoll(m);
+        if (v >= 64) {
+            c->max_props = v;
+            c->max_props_user = true;
+        }
+    }
+    if (const char* m = hook("LGS_SAMPLEZ_LIBM")) c->libm_samplez = atoi(m) != 0;
+    if (const char* m = hook("LGS_FAR")) c->oz_off = strcmp(m, "fp64") == 0;
     {
         // {erf(j/64), exp(-(j/64)^2)}, j = 0..kErfTabLast, rounded from long double.
         std::vector<double> tab(2 * (lgs::kErfTabLast + 1));
@@ -902,7 +986,7 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     c->z1seen = 0.0;
     c->z1cap = 0.0;
     for (size_t i = 0; i < dd; ++i) c->z1cap += 16.0 * co[2 * dd + i] + 4.0;
-    if (getenv("LGS_DEBUG_SZC")) {
+    if (hook("LGS_DEBUG_SZC")) {
         int hist[5] = {0, 0, 0, 0, 0};
         for (size_t i = 0; i < dd; ++i) hist[(int)szc[i * lgs::kSzcStride + 2]]++;
         fprintf(stderr, "lgs: SampleZ kinds round %d small %d closed %d capped %d generic %d\n", hist[0],
@@ -1166,7 +1250,7 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     // proposal block runs the C3 bench at 110 vs 105 M samples/s -- the launch's tail
     // and the per-block work amortised, profiles/r05aa_bench_ab.log)
     const int64_t cap = std::max<int64_t>(256, (int64_t)((size_t)32 << 30) / (8 * d));
-    if (!getenv("LGS_MAX_PROPOSALS")) c->max_props = std::min<int64_t>(std::max<int64_t>(cap, 256), 1 << 22);
+    if (!c->max_props_user) c->max_props = std::min<int64_t>(std::max<int64_t>(cap, 256), 1 << 22);
     return LGS_OK;
 }
 
@@ -1411,34 +1495,27 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
     // is enqueued while those run.  Not with the certified Wang-Ling accept (its
     // counters come from the accept kernel).  Timers of the later launches are folded
     // once they finish (fold_timers).  LGS_NO_EARLY_CHECK=1: A/B.
-    static const bool no_early = getenv("LGS_NO_EARLY_CHECK") && atoi(getenv("LGS_NO_EARLY_CHECK")) == 1;
+    static const bool no_early = hook_is("LGS_NO_EARLY_CHECK", 1);
     const bool early = dev && c->stream != c->own && !certw && !no_early;
     if (early && !c->fw_host) {
         HIP_TRY(hipHostMalloc((void**)&c->fw_host, 4 * lgs::kFlagWords, hipHostMallocDefault));
         HIP_TRY(hipEventCreateWithFlags(&c->fw_ev, hipEventDisableTiming));
     }
 
-    // ---- block of T steps (a multiple of thin) per Klein launch
-    int64_t T = std::max<int64_t>(1, c->max_props / nc);
-    if (T < n_steps) T = std::max<int64_t>(thin, (T / thin) * thin);
-    T = std::min<int64_t>(T, std::max<int64_t>(n_steps, 1));
-    const int64_t np = nc * T;
-    const int64_t kmax = std::max<int64_t>(T / thin, 1);
     // proposal store: np columns, plus nc columns for the chain states carried into a
     // block when lattice points are requested (kept-state selections become plain columns)
     const bool carry = v_samples != nullptr;
     // pipelined blocks (see lgs_ctx::BlockSet): the context's own store then only takes
-    // the initial draws (nc columns); LGS_NO_PIPE=1: A/B
-    static const bool no_pipe = getenv("LGS_NO_PIPE") && atoi(getenv("LGS_NO_PIPE")) == 1;
+    // the initial draws (nc columns); LGS_CTX_NO_PIPELINE: A/B
+    const bool no_pipe = c->no_pipe || hook_is("LGS_NO_PIPE", 1);
     const bool pipe = early && !no_pipe && n_steps > 0;
-    const int64_t own_cols = pipe ? nc : np + (carry ? nc : 0);
     if (pipe) {
         if (!c->kstream) {
             // LGS_PIPE_PRIO=1: at the device's highest priority, so the Klein launch's
             // workgroups are dispatched first (measured: no gain, 102.3-102.4 vs
             // 102.6-102.9 M samples/s at the default priority, profiles/r05k_*);
             // 2: at the lowest, so the previous block's dependants go first
-            static const int prio = getenv("LGS_PIPE_PRIO") ? atoi(getenv("LGS_PIPE_PRIO")) : 0;
+            static const int prio = hook("LGS_PIPE_PRIO") ? atoi(hook("LGS_PIPE_PRIO")) : 0;
             int plo = 0, phi = 0;
             if (prio && hipDeviceGetStreamPriorityRange(&plo, &phi) == hipSuccess && phi != plo)
                 HIP_TRY(hipStreamCreateWithPriority(&c->kstream, hipStreamNonBlocking, prio == 1 ? phi : plo));
@@ -1447,7 +1524,7 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             HIP_TRY(hipEventCreateWithFlags(&c->ev_klein, hipEventDisableTiming));
         }
         if (!c->kstream_sets_fixed) {
-            c->nsets = getenv("LGS_PIPE_SETS") && atoi(getenv("LGS_PIPE_SETS")) == 3 ? 3 : 2;
+            c->nsets = hook_is("LGS_PIPE_SETS", 3) ? 3 : 2;
             c->kstream_sets_fixed = true;
         }
         for (int si = 0; si < c->nsets; ++si) {
@@ -1457,15 +1534,63 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
                 if ((rc = s.flags.reserve(4 * lgs::kFlagWords))) return rc;
                 HIP_TRY(hipMemset(s.flags.p, 0, 4 * lgs::kFlagWords));
             }
-            // (a set in use by an earlier call's dependants is never grown here: the
-            // sizes depend on nc, T and d only, and hipFree waits for the device)
-            if ((rc = s.Z.reserve((size_t)(np + (carry ? nc : 0)) * d * std::max(zb, 4))) ||
-                (rc = s.LW.reserve((size_t)np * 8)))
-                return rc;
         }
     }
+    // ---- block of T steps (a multiple of thin) per Klein launch, and the device buffers
+    // of one block.  An allocation that fails halves the block (down to thin steps per
+    // chain; the smaller cap stays with the context) instead of returning LGS_ERR_NOMEM.
+    int64_t T = 1, np = 0, kmax = 1, own_cols = 0;
+    for (int64_t maxp = c->max_props;;) {
+        T = std::max<int64_t>(1, maxp / nc);
+        if (T < n_steps) T = std::max<int64_t>(thin, (T / thin) * thin);
+        T = std::min<int64_t>(T, std::max<int64_t>(n_steps, 1));
+        np = nc * T;
+        kmax = std::max<int64_t>(T / thin, 1);
+        own_cols = pipe ? nc : np + (carry ? nc : 0);
+        rc = LGS_OK;
+        // (a set in use by an earlier call's dependants is never grown here unless the
+        // sizes change -- they depend on nc, T and d only -- and hipFree waits for the device)
+        for (int si = 0; pipe && !rc && si < c->nsets; ++si) {
+            auto& s = c->bset[si];
+            if (!(rc = s.Z.reserve((size_t)(np + (carry ? nc : 0)) * d * std::max(zb, 4))) &&
+                !(rc = s.LW.reserve((size_t)np * 8)))
+                rc = reserve_oz(c, s.H16, s.ZNZ, s.CLIVE, np);
+        }
+        if (!rc && !(rc = c->Z.reserve((size_t)own_cols * d * std::max(zb, 4))) &&
+            !(rc = c->LW.reserve((size_t)(pipe ? nc : np) * 8)) &&
+            !(rc = c->sel.reserve((size_t)std::max<int64_t>(nc * kmax, nc) * 8)) &&
+            !(rc = c->fsel.reserve((size_t)nc * 8)) && !(rc = c->cnt.reserve((size_t)np * 4)) &&
+            !(rc = c->ccnt.reserve((size_t)nc * 4)) && !(certw && (rc = c->LWE.reserve((size_t)np * 8))))
+            rc = reserve_oz(c, c->H16, c->ZNZ, c->CLIVE, pipe ? nc : np);
+        if (rc != LGS_ERR_NOMEM || T <= thin || n_steps <= thin) {
+            if (rc) return rc;
+            break;
+        }
+        // release the block-sized buffers (a pending look-ahead writes into a set: drop it
+        // first) and retry at half the block
+        if ((rc = spec_discard(c))) return rc;
+        for (int si = 0; si < c->nsets; ++si) {
+            auto& s = c->bset[si];
+            s.Z.release();
+            s.LW.release();
+            s.H16.release();
+            s.ZNZ.release();
+            s.CLIVE.release();
+        }
+        c->Z.release();
+        c->LW.release();
+        c->cnt.release();
+        c->LWE.release();
+        c->H16.release();
+        c->ZNZ.release();
+        c->CLIVE.release();
+        c->hist = decltype(c->hist){};
+        maxp = std::max<int64_t>(nc * thin, maxp / 2);
+        c->max_props = maxp;
+        c->max_props_user = true;
+    }
     // the previous call's look-ahead launch: this call's first block if it matches
-    static const bool no_look = getenv("LGS_NO_LOOKAHEAD") && atoi(getenv("LGS_NO_LOOKAHEAD")) == 1;
+    const bool no_look = c->no_look || hook_is("LGS_NO_LOOKAHEAD", 1);
     bool spec_hit = false;
     if (c->spec.valid) {
         const int64_t tb0 = std::min<int64_t>(T, n_steps);
@@ -1475,12 +1600,6 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
                    sp.exact == exact && sp.j == c->bset_next;
         if (!spec_hit && (rc = spec_discard(c))) return rc;
     }
-    if ((rc = c->Z.reserve((size_t)own_cols * d * std::max(zb, 4))) ||
-        (rc = c->LW.reserve((size_t)(pipe ? nc : np) * 8)) ||
-        (rc = c->sel.reserve((size_t)std::max<int64_t>(nc * kmax, nc) * 8)) ||
-        (rc = c->fsel.reserve((size_t)nc * 8)) || (rc = c->cnt.reserve((size_t)np * 4)) ||
-        (rc = c->ccnt.reserve((size_t)nc * 4)) || (certw && (rc = c->LWE.reserve((size_t)np * 8))))
-        return rc;
 
     // ---- device views of the chain state (staged through device buffers for host pointers)
     void* zs = z_state;
@@ -1532,7 +1651,7 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
     // 101.7-102.9 M enqueued right behind the last Klein launch, whose dependants then
     // start later and hold the next launch's set longer, profiles/r05u_bench_ab.log);
     // LGS_LOOKAHEAD_EARLY=1: right behind it
-    static const bool look_late = !(getenv("LGS_LOOKAHEAD_EARLY") && atoi(getenv("LGS_LOOKAHEAD_EARLY")) == 1);
+    static const bool look_late = !hook_is("LGS_LOOKAHEAD_EARLY", 1);
     for (int64_t t0 = 0; t0 < n_steps || t0 == 0;) {
         bool oz_used = false;
         SetSwap sw;  // (pipe) this block's buffer set, swapped back on every exit
@@ -1591,6 +1710,7 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
         if (pipe && spec_hit && t0 == 0) {  // the previous call's look-ahead launch is this block's
             spec_hit = false;
             c->spec.valid = false;
+            for (auto& t : c->pending) t.spec = false;  // (its timers are this block's Klein launch)
             ozb = c->spec.oz;
             c->hist = c->spec.h;
             HIP_TRY(hipStreamWaitEvent(c->stream, c->spec.ev, 0));
@@ -1661,7 +1781,7 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             aa.flagw = fl;
             // test hook: widened bounds force the recomputation path on many decisions
             // (clamped to >= 1: a smaller scale would shrink the bounds and void the certificate)
-            const char* bs = getenv("LGS_TEST_WL_BOUND_SCALE");
+            const char* bs = hook("LGS_TEST_WL_BOUND_SCALE");
             aa.bscale = bs ? std::max(1.0, atof(bs)) : 1.0;
         }
         {
@@ -1678,10 +1798,11 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
         // them up.  A carried |z| beyond two digits (B z's digit-range flag) falls back to
         // the moments pass, gated on that flag on the device.  The chains' final states
         // then come from the int16 history.  LGS_NO_BZ_MOMENTS=1: the separate pass.
-        static const bool no_bz_mom = getenv("LGS_NO_BZ_MOMENTS") && atoi(getenv("LGS_NO_BZ_MOMENTS")) == 1;
-        static const bool bz_f64 = getenv("LGS_BZ_FP64") && atoi(getenv("LGS_BZ_FP64")) == 1;
+        static const bool no_bz_mom = hook_is("LGS_NO_BZ_MOMENTS", 1);
+        static const bool bz_f64 = hook_is("LGS_BZ_FP64", 1);
         const bool bz_mom = moments && v_samples && early && thin == 1 && kb == Tb && kb > 0 && zb == 2 &&
                             c->has_Bi8 && c->bz_mom_ok && !bz_f64 && c->hist.Z == c->Z.p && c->hist.Z &&
+                            c->hist.clive != nullptr && lgs::launch::bz_moments_supported() &&
                             d % 16 == 0 && d <= lgs::kOzMaxD && npb < ((int64_t)1 << 32) && !no_bz_mom;
         const bool fuse_final = !bz_mom && moments && !((z_samples || zk_samples) && kb > 0 && !carry) &&
                                 npb < ((int64_t)1 << 32);
@@ -1768,12 +1889,8 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
         bool redo = false;
         if ((rc = finish_or_redo(c, oz_used, zb, redo, early))) return rc;
         if (pipe) {  // the set's readers are all enqueued (its flag words reset behind them)
-            const int j = sw.j;
-            sw.restore();
-            sw.j = -1;
+            sw.release();
             fl = c->flags.as<unsigned int>();
-            HIP_TRY(hipEventRecord(c->bset[j].ev_free, c->stream));
-            c->bset[j].free_recorded = true;
             if (!redo) c->bset_next = (c->bset_next + 1) % c->nsets;
         }
         if (redo) continue;  // same block again (block 0: its initial draws too)

@@ -245,6 +245,16 @@ struct SeriesArgs {
 };
 
 namespace launch {
+// B z writes the kept states' moment partials (MP / MPL) on its clive path only: one
+// 64-sample tile per wave (LGS_BZ_TA == 1) and the Klein launch's per-wave chunk bits
+// (built by the rolled near field, not LGS_NEAR_UNROLLED; LGS_BZ_NO_CLIVE disables them)
+constexpr bool bz_moments_supported() {
+#if defined(LGS_BZ_NO_CLIVE) || defined(LGS_NEAR_UNROLLED) || (defined(LGS_BZ_TA) && LGS_BZ_TA != 1)
+    return false;
+#else
+    return true;
+#endif
+}
 // ---- diagnostics (lgs_diag.hip); xtype 0 fp64, 1 int32, 2 int64
 hipError_t series_stats(const SeriesArgs& a, hipStream_t st);
 // sum y y^T (d x d, both triangles) and sum y (d), y = x - shift (shift nullable),

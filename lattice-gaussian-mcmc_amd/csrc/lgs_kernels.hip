@@ -2171,6 +2171,7 @@ __global__ __launch_bounds__(64) void imhk_accept_cert_kernel(const AcceptArgs a
                                  (uint32_t)__builtin_amdgcn_readlane((int)cur, L);
             const int32_t sinitL = __builtin_amdgcn_readlane(sinit, L);
             double ly = 0.0, lx = 0.0;
+            int badx = 0;  // (the carried state's replay did not reproduce its z)
             if (eyL != 0.0)
                 ly = wl_exact_wave(ka, a.RT, (const char*)a.Zst + (cL * a.T + t) * a.zb, a.zb, a.ldz,
                                    a.step0 + (uint32_t)t, chL, true, bad);
@@ -2183,10 +2184,14 @@ __global__ __launch_bounds__(64) void imhk_accept_cert_kernel(const AcceptArgs a
                                        (const char*)a.zs + (a.zs_cm ? cL : cL * ka.d) * a.ob, a.ob,
                                        a.zs_cm ? a.nc : 1,
                                        sinitL >= kInitStep0 ? (uint32_t)(sinitL - kInitStep0) : 0u, chL,
-                                       sinitL >= kInitStep0, bad);
+                                       sinitL >= kInitStep0, badx);
             }
-            // a carried state replayed without its counters keeps a residual bound
-            const bool resid = exL != 0.0 && curL < 0 && sinitL < kInitStep0;
+            bad |= badx;
+            // a carried state replayed without its counters keeps a residual bound -- and so
+            // does one whose recorded step did not reproduce it (drawn under
+            // another seed or chain mapping, e.g. a resume with another seed)
+            const bool resid = exL != 0.0 && curL < 0 &&
+                               (sinitL < kInitStep0 || __builtin_amdgcn_ballot_w64(badx != 0) != 0);
             if (lane == L) {
                 if (eyL != 0.0) {
                     lw_y = ly;
@@ -3485,6 +3490,9 @@ hipError_t bz_i8(const void* Z, int zb, int64_t ldz, const int64_t* sel, const i
 #ifdef LGS_BZ_NO_CLIVE
     clive = nullptr;
 #endif
+    // the moment partials (MP / MPL) are written on the clive path only: never hand
+    // bz_moments_reduce partials this launch will not write
+    if (MP != nullptr && (clive == nullptr || !bz_moments_supported())) return hipErrorInvalidValue;
 #ifdef LGS_DIAG_BZ_NO_VNP  // diagnostic builds only: epilogue cost of the ||v||^2 partial sums
     VNP = nullptr;
 #endif

@@ -13,6 +13,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LGS_LIB") or os.path.join(_HERE, "_lib", "liblgs_hip.so")
+# the same sources built with -DLGS_TEST_HOOKS (the environment's test / A/B switches):
+# only tests that perturb the certificate on purpose use it (Context(hooks=True))
+HOOKS_LIB_PATH = os.path.join(_HERE, "_lib", "liblgs_hip_hooks.so")
 
 LGS_OK = 0
 LGS_ERR_INVALID = -1
@@ -36,6 +39,15 @@ LGS_LOGW_BOUND = 0x400
 LGS_X_I32 = 0x100
 LGS_X_I64 = 0x200
 
+# lgs_create_ex ctx_flags (include/lgs.h)
+LGS_CTX_NO_PIPELINE = 0x1
+LGS_CTX_NO_LOOKAHEAD = 0x2
+LGS_CTX_SAMPLEZ_LIBM = 0x4
+LGS_CTX_PANEL16 = 0x8
+LGS_CTX_FAR_FP64 = 0x10
+LGS_CTX_STORE32 = 0x20
+LGS_CTX_NO_QSKIP = 0x40
+
 KERNEL_KLEIN, KERNEL_BZ, KERNEL_ACCEPT, KERNEL_MOMENTS = 0, 1, 2, 3
 KERNEL_GRAM, KERNEL_SERIES, KERNEL_KLEIN_INIT = 4, 5, 6
 LGS_COUNTER_RESOLVED = 0
@@ -45,7 +57,7 @@ LGS_COUNTER_WL_MISMATCH = 3
 LGS_COUNTER_QSKIP = 4
 
 # every symbol include/lgs.h declares (checked by tests/test_capi_symbols.py)
-EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_destroy", "lgs_set_stream",
+EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_create_ex", "lgs_destroy", "lgs_set_stream",
            "lgs_set_basis", "lgs_klein", "lgs_imhk", "lgs_imhk_trace", "lgs_imhk_ex", "lgs_lattice_points", "lgs_log_density", "lgs_sample_z", "lgs_timing_enable",
            "lgs_timing_get", "lgs_device_info", "lgs_series_stats", "lgs_gram",
            "lgs_jump_distance", "lgs_marginal_tvd", "lgs_column_range", "lgs_histogram", "lgs_set_decoder", "lgs_nearest_plane",
@@ -67,7 +79,8 @@ class LgsError(RuntimeError):
         self.code = code
 
 
-_lib = None
+_lib = None   # the library at LIB_PATH (the product unless LGS_LIB names a variant)
+_libs = {}    # every library loaded, by path
 _vp = ctypes.c_void_p
 _dp = ctypes.POINTER(ctypes.c_double)
 _i32p = ctypes.POINTER(ctypes.c_int32)
@@ -77,8 +90,8 @@ _i64p = ctypes.POINTER(ctypes.c_int64)
 def load_library(path: str = LIB_PATH):
     """Load liblgs_hip.so (raises if it has not been built)."""
     global _lib
-    if _lib is not None:
-        return _lib
+    if path in _libs:
+        return _libs[path]
     # One HIP runtime per process: PyTorch ships its own libamdhip64 (soname
     # libamdhip64.so.7) and binds it by the unversioned name, so it must be
     # loaded first; liblgs_hip.so's NEEDED libamdhip64.so.7 then resolves to the
@@ -94,6 +107,8 @@ def load_library(path: str = LIB_PATH):
     L.lgs_version.restype = ctypes.c_int
     L.lgs_last_error.restype = ctypes.c_char_p
     L.lgs_create.argtypes = [ctypes.POINTER(_vp), ctypes.c_int]
+    if hasattr(L, "lgs_create_ex"):  # (round 6; older A/B baselines lack it)
+        L.lgs_create_ex.argtypes = [ctypes.POINTER(_vp), ctypes.c_int, ctypes.c_int64, ctypes.c_uint32]
     L.lgs_destroy.argtypes = [_vp]
     L.lgs_set_stream.argtypes = [_vp, _vp]
     L.lgs_set_basis.argtypes = [_vp, ctypes.c_int64, _dp, _dp, _dp, ctypes.c_double, ctypes.c_int32,
@@ -133,13 +148,15 @@ def load_library(path: str = LIB_PATH):
     for name in EXPORTS:
         if name not in ("lgs_version", "lgs_last_error") and hasattr(L, name):
             getattr(L, name).restype = ctypes.c_int
-    _lib = L
+    _libs[path] = L
+    if path == LIB_PATH:
+        _lib = L
     return L
 
 
-def _check(rc):
+def _check(rc, L=None):
     if rc != LGS_OK:
-        msg = _lib.lgs_last_error().decode(errors="replace")
+        msg = (L or _lib or load_library()).lgs_last_error().decode(errors="replace")
         raise LgsError(rc, msg)
 
 
@@ -198,17 +215,36 @@ def x_flags(a) -> int:
 class Context:
     """One HIP device context (stream + device-resident basis + scratch)."""
 
-    def __init__(self, device: int = 0):
-        L = load_library()
+    def __init__(self, device: int = 0, *, max_proposals: int = 0, pipeline: bool = True,
+                 lookahead: bool = True, samplez_libm: bool = False, panel: int = 32, far: str = "int8",
+                 store32: bool = False, qskip: bool = True, hooks: bool = False):
+        """lgs_create_ex: max_proposals (0 = the library's default) and the LGS_CTX_*
+        options; hooks=True loads liblgs_hip_hooks.so (the environment's test switches)."""
+        L = load_library(HOOKS_LIB_PATH if hooks else LIB_PATH)
+        self._L = L
+        flags = ((0 if pipeline else LGS_CTX_NO_PIPELINE) | (0 if lookahead else LGS_CTX_NO_LOOKAHEAD) |
+                 (LGS_CTX_SAMPLEZ_LIBM if samplez_libm else 0) | (LGS_CTX_PANEL16 if panel == 16 else 0) |
+                 (LGS_CTX_FAR_FP64 if far == "fp64" else 0) | (LGS_CTX_STORE32 if store32 else 0) |
+                 (0 if qskip else LGS_CTX_NO_QSKIP))
+        if panel not in (16, 32) or far not in ("int8", "fp64"):
+            raise ValueError("panel is 16 or 32, far is 'int8' or 'fp64'")
         h = _vp()
-        _check(L.lgs_create(ctypes.byref(h), int(device)))
+        if hasattr(L, "lgs_create_ex"):
+            _check(L.lgs_create_ex(ctypes.byref(h), int(device), int(max_proposals), flags), L)
+        elif flags or max_proposals:
+            raise LgsError(LGS_ERR_INVALID, "this library build has no lgs_create_ex")
+        else:
+            _check(L.lgs_create(ctypes.byref(h), int(device)), L)
         self._h = h
         self.device = device
         self.d = 0
 
+    def _ck(self, rc):
+        _check(rc, self._L)
+
     def close(self):
-        if getattr(self, "_h", None) and _lib is not None:
-            _lib.lgs_destroy(self._h)
+        if getattr(self, "_h", None) and getattr(self, "_L", None) is not None:
+            self._L.lgs_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -216,7 +252,7 @@ class Context:
 
     # ---------------------------------------------------------------- setup
     def set_stream(self, stream_handle):
-        _check(_lib.lgs_set_stream(self._h, _vp(stream_handle) if stream_handle else None))
+        self._ck(self._L.lgs_set_stream(self._h, _vp(stream_handle) if stream_handle else None))
 
     def set_basis(self, R, cprime, B, sigma, precision=10, linear_probs=False):
         R = np.ascontiguousarray(R, dtype=np.float64)
@@ -226,7 +262,7 @@ class Context:
         if R.shape != (d, d) or cp.shape != (d,) or (Bc is not None and Bc.shape != (d, d)):
             raise ValueError("shape mismatch between R, cprime and B")
         flags = LGS_BASIS_LINEAR_PROBS if linear_probs else 0
-        _check(_lib.lgs_set_basis(self._h, d, R.ctypes.data_as(_dp), cp.ctypes.data_as(_dp),
+        self._ck(self._L.lgs_set_basis(self._h, d, R.ctypes.data_as(_dp), cp.ctypes.data_as(_dp),
                                   None if Bc is None else Bc.ctypes.data_as(_dp), float(sigma),
                                   int(precision), flags))
         self.d = d
@@ -238,7 +274,7 @@ class Context:
         zt = "int64" if flags & LGS_Z64 else "int32"
         _check_bufs(flags, self.device, ((z_out, zt, "z_out"), (v_out, "float64", "v_out"),
                                          (logw_out, "float64", "logw_out")))
-        _check(_lib.lgs_klein(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(first), int(n),
+        self._ck(self._L.lgs_klein(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(first), int(n),
                               _ptr(z_out), _ptr(v_out), _ptr(logw_out), int(flags)))
 
     def klein_host(self, seed, first, n, *, want_z=True, want_v=True, want_logw=False, flags=0):
@@ -291,11 +327,11 @@ class Context:
                                                  (lg[3], "float64", "lag v ring"), (lg[4], "float64", "lag v sums")))
             out = ImhkOutputs(v(logw_samples), v(accepted), v(vnorm2_samples), v(zk_samples), int(zk_index),
                               int(fn_chains), int(lg[0]), v(lg[1]), v(lg[2]), v(lg[3]), v(lg[4]), float(lg[5]))
-            _check(_lib.lgs_imhk_ex(*args, ctypes.byref(out), int(flags)))
+            self._ck(self._L.lgs_imhk_ex(*args, ctypes.byref(out), int(flags)))
         elif logw_samples is None and accepted is None:
-            _check(_lib.lgs_imhk(*args, int(flags)))
+            self._ck(self._L.lgs_imhk(*args, int(flags)))
         else:
-            _check(_lib.lgs_imhk_trace(*args, _ptr(logw_samples), _ptr(accepted), int(flags)))
+            self._ck(self._L.lgs_imhk_trace(*args, _ptr(logw_samples), _ptr(accepted), int(flags)))
 
     def lattice_points(self, z, v_out=None, flags=0):
         if isinstance(z, np.ndarray):
@@ -303,11 +339,11 @@ class Context:
             zz = np.ascontiguousarray(z, dtype=np.int64 if z64 else np.int32)
             n = zz.shape[0]
             v = np.empty((n, self.d)) if v_out is None else v_out
-            _check(_lib.lgs_lattice_points(self._h, n, _ptr(zz), _ptr(v),
+            self._ck(self._L.lgs_lattice_points(self._h, n, _ptr(zz), _ptr(v),
                                            int(flags | (LGS_Z64 if z64 else 0))))
             return v
         n = z.shape[0] if not (flags & LGS_COORD_MAJOR) else z.shape[1]
-        _check(_lib.lgs_lattice_points(self._h, n, _ptr(z), _ptr(v_out), int(flags)))
+        self._ck(self._L.lgs_lattice_points(self._h, n, _ptr(z), _ptr(v_out), int(flags)))
         return v_out
 
     def log_density(self, z):
@@ -316,7 +352,7 @@ class Context:
         if not z64:
             zz = zz.astype(np.int32)
         out = np.empty(zz.shape[0])
-        _check(_lib.lgs_log_density(self._h, zz.shape[0], _ptr(zz), _ptr(out),
+        self._ck(self._L.lgs_log_density(self._h, zz.shape[0], _ptr(zz), _ptr(out),
                                     LGS_Z64 if z64 else 0))
         return out
 
@@ -329,7 +365,7 @@ class Context:
         f = (LGS_SAMPLEZ_TABLE if table else 0) | (LGS_BASIS_LINEAR_PROBS if linear_probs else 0)
         f |= {None: 0, "decision": LGS_SAMPLEZ_DECISION, "libm": LGS_SAMPLEZ_LIBM,
               "libm_decision": LGS_SAMPLEZ_LIBM | LGS_SAMPLEZ_DECISION}[mode]
-        _check(_lib.lgs_sample_z(self._h, mu.size, _ptr(mu), _ptr(sg), _ptr(uu), int(precision),
+        self._ck(self._L.lgs_sample_z(self._h, mu.size, _ptr(mu), _ptr(sg), _ptr(uu), int(precision),
                                  _ptr(z), _ptr(ln), f))
         return z, ln
 
@@ -340,14 +376,14 @@ class Context:
         for M in (Qc, Bi):
             if M is not None and M.shape != (self.d, self.d):
                 raise ValueError("decoder matrices must be d x d")
-        _check(_lib.lgs_set_decoder(self._h, _ptr(Qc), _ptr(Bi)))
+        self._ck(self._L.lgs_set_decoder(self._h, _ptr(Qc), _ptr(Bi)))
         self._keep_dec = (Qc, Bi)
 
     def decode(self, targets, method="plane", z_out=None, v_out=None, flags=0):
         """Raw lgs_nearest_plane / lgs_round_decode on caller buffers."""
-        fn = _lib.lgs_nearest_plane if method == "plane" else _lib.lgs_round_decode
+        fn = self._L.lgs_nearest_plane if method == "plane" else self._L.lgs_round_decode
         n = targets.shape[1] if flags & LGS_COORD_MAJOR else targets.shape[0]
-        _check(fn(self._h, int(n), _ptr(targets), _ptr(z_out), _ptr(v_out), int(flags)))
+        self._ck(fn(self._h, int(n), _ptr(targets), _ptr(z_out), _ptr(v_out), int(flags)))
 
     def decode_host(self, targets, method="plane", want_v=True):
         """Decode host targets (n x d); int32 coefficients first, int64 on overflow."""
@@ -371,7 +407,7 @@ class Context:
                      tau=None, batch_means=None, flags=0):
         """Raw lgs_series_stats; x / outputs are host arrays or device tensors
         (flags must then carry LGS_DEVICE_PTRS); element type via x_flags(x)."""
-        _check(_lib.lgs_series_stats(self._h, _ptr(x), int(n_series), int(n), int(group_size),
+        self._ck(self._L.lgs_series_stats(self._h, _ptr(x), int(n_series), int(n), int(group_size),
                                      int(group_stride), int(series_stride), int(time_stride),
                                      int(max_lag), float(window_c), int(batch_size), _ptr(mean),
                                      _ptr(c0), _ptr(acf), _ptr(tau), _ptr(batch_means),
@@ -385,25 +421,25 @@ class Context:
             d, n = x.shape
         else:
             n, d = x.shape
-        _check(_lib.lgs_gram(self._h, int(d), int(n), _ptr(x), int(n if coord_major else d),
+        self._ck(self._L.lgs_gram(self._h, int(d), int(n), _ptr(x), int(n if coord_major else d),
                              _ptr(shift), _ptr(sum_out), _ptr(gram_out), int(f)))
 
     def jump_distance(self, x, out, flags=0):
         n, d = x.shape
-        _check(_lib.lgs_jump_distance(self._h, int(n), int(d), _ptr(x), int(d), _ptr(out),
+        self._ck(self._L.lgs_jump_distance(self._h, int(n), int(d), _ptr(x), int(d), _ptr(out),
                                       int(flags | x_flags(x))))
 
     def marginal_tvd(self, x1, x2, out, flags=0):
         if _dtype_name(x1) != _dtype_name(x2):
             raise TypeError("both sample sets must have the same dtype")
         d = x1.shape[1]
-        _check(_lib.lgs_marginal_tvd(self._h, int(d), _ptr(x1), int(x1.shape[0]), _ptr(x2),
+        self._ck(self._L.lgs_marginal_tvd(self._h, int(d), _ptr(x1), int(x1.shape[0]), _ptr(x2),
                                      int(x2.shape[0]), _ptr(out), int(flags | x_flags(x1))))
 
     def column_range(self, x, lo, hi, flags=0):
         """Per-column min / max (fp64) of row-major (n, d) samples into lo / hi (d)."""
         n, d = x.shape
-        _check(_lib.lgs_column_range(self._h, int(d), _ptr(x), int(n), _ptr(lo), _ptr(hi),
+        self._ck(self._L.lgs_column_range(self._h, int(d), _ptr(x), int(n), _ptr(lo), _ptr(hi),
                                      int(flags | x_flags(x))))
 
     def histogram(self, x, edges, first_denom, counts, flags=0):
@@ -416,43 +452,43 @@ class Context:
             raise ValueError("histogram: edges (d, bins+1), first_denom (d, 2), counts (d, bins)")
         _check_bufs(flags, self.device, ((edges, "float64", "edges"), (first_denom, "float64", "first_denom"),
                                          (counts, "int64", "counts")))
-        _check(_lib.lgs_histogram(self._h, int(d), _ptr(x), int(n), int(bins), _ptr(edges),
+        self._ck(self._L.lgs_histogram(self._h, int(d), _ptr(x), int(n), int(bins), _ptr(edges),
                                   _ptr(first_denom), _ptr(counts), int(flags | x_flags(x))))
 
     # ---------------------------------------------------------------- timing / info
     def timing_enable(self, on=True):
-        _check(_lib.lgs_timing_enable(self._h, 1 if on else 0))
+        self._ck(self._L.lgs_timing_enable(self._h, 1 if on else 0))
 
     def timing_get(self, kernel):
         ms = ctypes.c_double(0)
         n = ctypes.c_int64(0)
-        _check(_lib.lgs_timing_get(self._h, int(kernel), ctypes.byref(ms), ctypes.byref(n)))
+        self._ck(self._L.lgs_timing_get(self._h, int(kernel), ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
     def resolved(self, reset=False):
         """Decisions the certificate did not cover and that were redone at the
         reference-order mean (LGS_COUNTER_RESOLVED), since creation / the last reset."""
         v = ctypes.c_uint64(0)
-        _check(_lib.lgs_counter(self._h, LGS_COUNTER_RESOLVED, 1 if reset else 0, ctypes.byref(v)))
+        self._ck(self._L.lgs_counter(self._h, LGS_COUNTER_RESOLVED, 1 if reset else 0, ctypes.byref(v)))
         return v.value
 
     def fallbacks(self, reset=False):
         """Klein launches redone with a wider store / the fp64 far field (LGS_COUNTER_FALLBACK)."""
         v = ctypes.c_uint64(0)
-        _check(_lib.lgs_counter(self._h, LGS_COUNTER_FALLBACK, 1 if reset else 0, ctypes.byref(v)))
+        self._ck(self._L.lgs_counter(self._h, LGS_COUNTER_FALLBACK, 1 if reset else 0, ctypes.byref(v)))
         return v.value
 
     def counter(self, which, reset=False):
         """lgs_counter: one of the LGS_COUNTER_* event counts since creation / the last reset."""
         v = ctypes.c_uint64(0)
-        _check(_lib.lgs_counter(self._h, int(which), 1 if reset else 0, ctypes.byref(v)))
+        self._ck(self._L.lgs_counter(self._h, int(which), 1 if reset else 0, ctypes.byref(v)))
         return v.value
 
     def device_info(self):
         buf = ctypes.create_string_buffer(256)
         ncu = ctypes.c_int(0)
         mem = ctypes.c_int64(0)
-        _check(_lib.lgs_device_info(self._h, buf, 256, ctypes.byref(ncu), ctypes.byref(mem)))
+        self._ck(self._L.lgs_device_info(self._h, buf, 256, ctypes.byref(ncu), ctypes.byref(mem)))
         return {"name": buf.value.decode(), "n_cu": ncu.value, "hbm_bytes": mem.value}
 
 

@@ -34,6 +34,33 @@ def test_library_exports_every_declared_symbol():
     assert L.lgs_version() == 100
 
 
+def test_product_library_reads_no_environment():
+    """Test and A/B switches exist only in the -DLGS_TEST_HOOKS build: the product
+    library does not import getenv at all (nothing in a user's environment
+    changes what it computes); the hooks library does, and exports the same ABI."""
+    import subprocess
+    from lgs_amd import _capi
+
+    def undefined(path):
+        out = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True, text=True, check=True)
+        return {ln.split()[-1].split("@")[0] for ln in out.stdout.splitlines() if ln.strip()}
+
+    prod = os.path.join(os.path.dirname(_capi.__file__), "_lib", "liblgs_hip.so")
+    assert "getenv" not in undefined(prod)
+    assert "getenv" in undefined(_capi.HOOKS_LIB_PATH)
+    H = ctypes.CDLL(_capi.HOOKS_LIB_PATH)
+    for s in declared_symbols():
+        assert hasattr(H, s), f"{s} missing from the hooks library"
+
+
+def test_context_options_validated():
+    from lgs_amd import _capi
+    with pytest.raises(ValueError):
+        _capi.Context(0, panel=24)
+    with pytest.raises(ValueError):
+        _capi.Context(0, far="fp32")
+
+
 def test_library_is_gfx950_code_object():
     from lgs_amd import _capi
     blob = open(_capi.LIB_PATH, "rb").read()

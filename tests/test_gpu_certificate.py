@@ -120,11 +120,11 @@ def test_low_z1_cap_forces_verification_not_speculation(capi, oracle, scale, mon
     q-coordinates.  Output must equal the reference-order kernel's."""
     import torch
     from lgs_amd import lattices
-    if scale != 1.0:
+    if scale != 1.0:  # (a test hook: liblgs_hip_hooks.so reads it, the product library has none)
         monkeypatch.setenv("LGS_TEST_Z1CAP_SCALE", str(scale))
     B = lattices.ntru_basis(128, 12289, 3)
     R, cp = oracle.qr_prepare(B)
-    ctx = capi.Context(0)
+    ctx = capi.Context(0, hooks=scale != 1.0)
     ctx.set_basis(R, cp, B, 165.7)
     d = B.shape[0]
     f = capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR
@@ -152,7 +152,7 @@ def test_q_panel_skip_equals_full_computation(capi, oracle, cfg, center_scale, m
     """Reference mode skips a panel of speculative (tiny-sigma) rows when the host's
     Cauchy-Schwarz bound on every row's mean, from ||z_W|| of the sample, certifies
     z = 0 there (lgs_set_basis, klein_mfma_kernel).  z must equal the launch that
-    computes those panels (LGS_NO_QSKIP=1) and the reference-order kernel; the weights
+    computes those panels (LGS_CTX_NO_QSKIP) and the reference-order kernel; the weights
     differ by the rows' mean-dependent rounding only (the terms are lterm at mu = 0).
     A center of scale ~q moves the means off 0: the bound fails and nothing is skipped."""
     import torch
@@ -165,8 +165,7 @@ def test_q_panel_skip_equals_full_computation(capi, oracle, cfg, center_scale, m
     n = 1 << 14 if d <= 1024 else 1 << 12
     out = {}
     for skip in ("0", "1"):
-        monkeypatch.setenv("LGS_NO_QSKIP", skip)
-        ctx = capi.Context(0)
+        ctx = capi.Context(0, qskip=skip == "0")
         ctx.set_basis(R, cp, B, sigma)
         z = torch.empty((d, n), dtype=torch.int32, device="cuda")
         lw = torch.empty(n, dtype=torch.float64, device="cuda")

@@ -138,9 +138,7 @@ def test_zero_vector_reductions_and_decodes(ctx, oracle):
 def test_imhk_16bit_store_with_wide_carried_states(capi, oracle):
     """The default 16-bit proposal store receives the chain states through the carry
     columns; caller-supplied states beyond int16 switch it to 32 bits, so lattice
-    points, moments and final states are those of a 32-bit store (LGS_ZINT=4)."""
-    import os
-
+    points, moments and final states are those of a 32-bit store (LGS_CTX_STORE32)."""
     import torch
     d, nc, T = 40, 64, 6
     B = _int_basis(d, 5)
@@ -149,11 +147,7 @@ def test_imhk_16bit_store_with_wide_carried_states(capi, oracle):
     z0[:, 0] = 50000
     z0[3, 5] = -70000
     for zint in ("2", "4"):
-        os.environ["LGS_ZINT"] = zint
-        try:
-            c = capi.Context(0)
-        finally:
-            del os.environ["LGS_ZINT"]
+        c = capi.Context(0, store32=zint == "4")
         c.set_basis(R, cp, B, 3.0)
         dev = "cuda:0"
         z = torch.from_numpy(z0.copy()).to(dev)

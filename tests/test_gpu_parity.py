@@ -70,11 +70,7 @@ def test_klein_matches_oracle_seeded(ctx, oracle, case, mode):
 @pytest.fixture(scope="module")
 def ctx_libm(capi):
     """A context on the generic SampleZ path (ocml erf/exp/erfinv, no per-coordinate constants)."""
-    os.environ["LGS_SAMPLEZ_LIBM"] = "1"
-    try:
-        return capi.Context(0)
-    finally:
-        del os.environ["LGS_SAMPLEZ_LIBM"]
+    return capi.Context(0, samplez_libm=True)
 
 
 def _wide_sigma_basis(d, seed):
@@ -111,11 +107,7 @@ def test_klein_coord_constants_vs_generic_samplez(ctx, ctx_libm, oracle, capi, p
 @pytest.fixture(scope="module")
 def ctx_far64(capi):
     """A context whose 32-row-panel kernel uses the fp64 MFMA far field."""
-    os.environ["LGS_FAR"] = "fp64"
-    try:
-        return capi.Context(0)
-    finally:
-        del os.environ["LGS_FAR"]
+    return capi.Context(0, far="fp64")
 
 
 def test_int8_digit_far_field_matches_fp64_far_field(ctx, ctx_far64, oracle):
@@ -213,17 +205,12 @@ def test_klein_batch_and_offset_invariance(ctx):
 
 
 def test_small_launch_chunks_and_panel16(capi, oracle):
-    """Chunked launches (LGS_MAX_PROPOSALS) and the 16-row panel give identical z."""
+    """Chunked launches (max_proposals) and the 16-row panel give identical z."""
     g = load_golden("klein_qary128.npz")
     R, cp, B = golden_R(g)
-    os.environ["LGS_MAX_PROPOSALS"] = "100"
-    os.environ["LGS_PANEL"] = "16"
-    try:
-        c2 = capi.Context(0)
-        c2.set_basis(R, cp, B, float(g["sigma"]))
-        r = c2.klein_host(int(g["seed"]), 0, int(g["n"]), want_z=True, want_v=True)
-    finally:
-        del os.environ["LGS_MAX_PROPOSALS"], os.environ["LGS_PANEL"]
+    c2 = capi.Context(0, max_proposals=100, panel=16)
+    c2.set_basis(R, cp, B, float(g["sigma"]))
+    r = c2.klein_host(int(g["seed"]), 0, int(g["n"]), want_z=True, want_v=True)
     assert np.array_equal(r["z"], g["z"])
     assert np.array_equal(r["v"], g["v"])
 
@@ -330,13 +317,9 @@ def test_imhk_matches_oracle(ctx, oracle, capi, wl):
 def test_imhk_block_split_invariance(capi):
     g = load_golden("klein_ntru128.npz")
     R, cp, B = golden_R(g)
-    os.environ["LGS_MAX_PROPOSALS"] = "200"
-    try:
-        c2 = capi.Context(0)
-        st_a, zs_a, mom_a = _imhk_dev(c2, R, cp, B, float(g["sigma"]), 16, 40, 31, thin=2,
-                                      flags=capi.LGS_WANG_LING, moments=True)
-    finally:
-        del os.environ["LGS_MAX_PROPOSALS"]
+    c2 = capi.Context(0, max_proposals=200)
+    st_a, zs_a, mom_a = _imhk_dev(c2, R, cp, B, float(g["sigma"]), 16, 40, 31, thin=2,
+                                  flags=capi.LGS_WANG_LING, moments=True)
     c3 = capi.Context(0)
     st_b, zs_b, mom_b = _imhk_dev(c3, R, cp, B, float(g["sigma"]), 16, 40, 31, thin=2,
                                   flags=capi.LGS_WANG_LING, split=[10, 30], moments=True)

@@ -374,7 +374,7 @@ def test_early_check_equals_synchronised_call(capi, zmax):
 
 def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, blocks: int = 3, plan=None,
                 thin: int = 1, z64: bool = False):
-    """Several lgs_imhk_ex calls of several blocks each (LGS_MAX_PROPOSALS: T = 4 steps
+    """Several lgs_imhk_ex calls of several blocks each (max_proposals: T = 4 steps
     per block), chain state, accept counts, moments, lattice points, functionals and
     lag sums carried across them -- on a caller's stream the blocks are pipelined
     (each block's Klein launch on the context's Klein stream into alternating buffer
@@ -384,15 +384,7 @@ def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, 
     g = load_golden("klein_qary128.npz")
     R, cp, B = golden_R(g)
     d, nc, T = R.shape[0], 256, 4
-    old = os.environ.get("LGS_MAX_PROPOSALS")
-    os.environ["LGS_MAX_PROPOSALS"] = str(nc * T)
-    try:
-        ctx = capi.Context(0)
-    finally:
-        if old is None:
-            del os.environ["LGS_MAX_PROPOSALS"]
-        else:
-            os.environ["LGS_MAX_PROPOSALS"] = old
+    ctx = capi.Context(0, max_proposals=nc * T)
     ctx.set_basis(R, cp, B, float(g["sigma"]))
     dev = "cuda:0"
     plan = plan or [T * blocks] * calls  # steps per call (a changed count discards the look-ahead launch)
@@ -517,3 +509,49 @@ def test_lookahead_discarded_on_new_basis_and_changed_call(capi):
     # v = B z for the fresh basis (not the look-ahead's)
     zrec = np.rint(np.linalg.solve(Bb.astype(np.float64), got[0].reshape(-1, d).T)).T
     assert np.array_equal(Bb.astype(np.float64) @ zrec.T, got[0].reshape(-1, d).T)
+
+
+def test_pipelined_call_error_then_next_call(capi):
+    """a pipelined call that ends in an error (here LGS_ERR_OVERFLOW:
+    |z| beyond the int32 state at sigma = 1e12) leaves its block's readers enqueued on
+    the caller's stream; the set's free event is recorded on that exit too, so the next
+    call's Klein launch into the same buffer set waits for them.  The next call (int64
+    state) equals the same call on a fresh context."""
+    import torch
+    d, nc, T = 16, 256, 4
+    B = np.eye(d)
+    R, cp = np.eye(d), np.zeros(d)
+    dev = "cuda:0"
+    ctx, ref = capi.Context(0, max_proposals=nc * T), capi.Context(0, max_proposals=nc * T)
+
+    def state(dt):
+        return dict(z=torch.zeros((d, nc), dtype=dt, device=dev), lw=torch.zeros(nc, dtype=torch.float64, device=dev),
+                    init=torch.zeros(nc, dtype=torch.int32, device=dev),
+                    acc=torch.zeros(nc, dtype=torch.int64, device=dev),
+                    mom=torch.zeros(2 * d, dtype=torch.int64, device=dev))
+
+    def call(c, st, flags):
+        v = torch.zeros((nc, 3 * T, d), dtype=torch.float64, device=dev)
+        c.imhk(5, 0, nc, 1, 3 * T, 1, st["z"], st["lw"], st["init"], st["acc"], v_samples=v, moments=st["mom"],
+               flags=capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR | flags)
+        return v
+
+    out = []
+    for c, pipelined in ((ctx, True), (ref, False)):
+        c.set_basis(R, cp, B, 1e12)
+        s = torch.cuda.Stream(device=dev)
+        torch.cuda.synchronize()
+        if pipelined:
+            c.set_stream(s.cuda_stream)
+        with torch.cuda.stream(s):
+            if pipelined:
+                with pytest.raises(capi.LgsError):
+                    call(c, state(torch.int32), 0)
+            st = state(torch.int64)
+            v = call(c, st, capi.LGS_Z64)
+        torch.cuda.synchronize()
+        out.append([v.cpu().numpy(), st["z"].cpu().numpy(), st["acc"].cpu().numpy(), st["lw"].cpu().numpy()])
+        c.close()
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    assert np.abs(out[0][1]).max() > 2 ** 31  # the int64 states hold what the int32 call could not

@@ -61,7 +61,7 @@ def test_wl_accept_flags_equal_exact_order(capi, oracle, c3, scale, calls, monke
     B, R, cp, sigma = c3
     d = B.shape[0]
     nc, T, seed = 1 << 14, 64, 4099
-    ctx = capi.Context(0)
+    ctx = capi.Context(0, hooks=scale != 1.0)  # (the bound scale is a test hook of liblgs_hip_hooks.so)
     ctx.set_basis(R, cp, B, sigma)
     zx, lwx, accx, fx, ix = _run(capi, ctx, d, nc, T, seed, capi.LGS_EXACT_ORDER)
     if scale != 1.0:
