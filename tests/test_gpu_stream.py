@@ -513,14 +513,14 @@ def test_lookahead_discarded_on_new_basis_and_changed_call(capi):
 
 def test_pipelined_call_error_then_next_call(capi):
     """a pipelined call that ends in an error (here LGS_ERR_OVERFLOW:
-    |z| beyond the int32 state at sigma = 1e12) leaves its block's readers enqueued on
+    |z| beyond the int32 state: a center of 3e9 on Z^16) leaves its block's readers enqueued on
     the caller's stream; the set's free event is recorded on that exit too, so the next
     call's Klein launch into the same buffer set waits for them.  The next call (int64
     state) equals the same call on a fresh context."""
     import torch
     d, nc, T = 16, 256, 4
     B = np.eye(d)
-    R, cp = np.eye(d), np.zeros(d)
+    R, cp = np.eye(d), np.full(d, 3.0e9)
     dev = "cuda:0"
     ctx, ref = capi.Context(0, max_proposals=nc * T), capi.Context(0, max_proposals=nc * T)
 
@@ -538,7 +538,7 @@ def test_pipelined_call_error_then_next_call(capi):
 
     out = []
     for c, pipelined in ((ctx, True), (ref, False)):
-        c.set_basis(R, cp, B, 1e12)
+        c.set_basis(R, cp, B, 3.0)
         s = torch.cuda.Stream(device=dev)
         torch.cuda.synchronize()
         if pipelined:
