@@ -95,6 +95,21 @@ __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
         const uint32_t lo1 = 0xCD9E8D57u * c2;
         const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
 #endif
+#ifndef LGS_PHILOX_NO_BITOP3
+        if (OPAQUE && r >= 2) {
+            // from the third round every word is per-lane: each three-way xor in one gfx950
+            // v_bitop3_b32 (truth table 0x96) instead of two v_xor_b32 -- 16 VALU fewer per
+            // block, the same bits (the first two rounds mix scalar words: s_xor + v_xor)
+            uint32_t n0, n2;
+            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c1), "s"(k0));
+            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c3), "s"(k1));
+            c0 = n0;
+            c1 = lo1;
+            c2 = n2;
+            c3 = lo0;
+            continue;
+        }
+#endif
         const uint32_t n0 = hi1 ^ c1 ^ k0;
         const uint32_t n2 = hi0 ^ c3 ^ k1;
         c0 = n0;

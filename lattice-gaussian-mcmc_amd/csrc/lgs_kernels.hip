@@ -189,9 +189,23 @@ __device__ __forceinline__ RecRegs load_rec(lds_cdptr rec, MID mid = MID{}) {
 #ifdef LGS_CAP_RI_PRE
     r.ri = load_cap_ri();
 #endif
-#ifndef LGS_REC_NOPIN
     // pinned here: left alone, the compiler sinks each read into the branch that
-    // uses it (three round trips after the kind / window branches)
+    // uses it (three round trips after the kind / window branches).
+#if !defined(LGS_REC_NOPIN) && !defined(LGS_REC_L2) && defined(LGS_REC_PIN_BATCH)
+    // (LGS_REC_PIN_BATCH: two asm statements over 22 registers each, one wait for the
+    // batch instead of one s_waitcnt lgkmcnt(k) per register -- the allocator then
+    // adds ~9 v_mov_b64 copies per step)
+    static_assert(kRecHot == 44, "two pins of 22");
+#define LGS_PIN22(o)                                                                                         \
+    asm volatile("" : "+v"(r.v[o + 0]), "+v"(r.v[o + 1]), "+v"(r.v[o + 2]), "+v"(r.v[o + 3]), "+v"(r.v[o + 4]),   \
+                 "+v"(r.v[o + 5]), "+v"(r.v[o + 6]), "+v"(r.v[o + 7]), "+v"(r.v[o + 8]), "+v"(r.v[o + 9]),        \
+                 "+v"(r.v[o + 10]), "+v"(r.v[o + 11]), "+v"(r.v[o + 12]), "+v"(r.v[o + 13]), "+v"(r.v[o + 14]),   \
+                 "+v"(r.v[o + 15]), "+v"(r.v[o + 16]), "+v"(r.v[o + 17]), "+v"(r.v[o + 18]), "+v"(r.v[o + 19]),   \
+                 "+v"(r.v[o + 20]), "+v"(r.v[o + 21]))
+    LGS_PIN22(0);
+    LGS_PIN22(22);
+#undef LGS_PIN22
+#elif !defined(LGS_REC_NOPIN)
 #pragma unroll
     for (int k = 0; k < kRecHot; ++k)
 #ifdef LGS_REC_L2  // (Rs[1..14] not pinned: the first use waits for them)
@@ -913,6 +927,13 @@ struct ZQuad<int64_t> {
 // VGPRs.  Row tile 1 (the upper sub-panel) goes to acc through the LDS tile;
 // tile 0 is parked in the per-wave scratch f0 and moved into the LDS tile once
 // the upper rows are loaded (the LDS tile is free during the upper sub-panel).
+#ifdef LGS_DIAG_FAR  // diagnostic builds only: per-wave shader-clock phases of the far field's chunk loop
+__device__ unsigned long long lgs_diag_far[8];  // [0] history wait [1] slab store [2] MFMA issue [3] barrier
+                                                // [4] prologue [5] epilogue [6] chunk visits [7] calls
+#define LGS_DF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define LGS_DF_T(v)
+#endif
 #ifndef LGS_OZ_NG  // 16-sample groups per far-field pass (1 or 2)
 #define LGS_OZ_NG 2
 #endif
@@ -956,18 +977,160 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
         for (int reg = 0; reg < 4; ++reg) t1v[g][reg] = 0.0;
 #endif
     auto slab_load = [&](int ch, v4i32_t (&pf)[4]) {
+#ifdef LGS_DIAG_FAR_NOSLAB
+        ch = 0;
+#endif
         const v4i32_t* src = rsrc + (size_t)ch * SLAB;
 #pragma unroll
         for (int m = 0; m < 4; ++m)
             if (tid + 256 * m < SLAB) pf[m] = src[tid + 256 * m];
     };
     auto slab_store = [&](int buf, const v4i32_t (&pf)[4]) {
+#ifdef LGS_DIAG_FAR_NOSLAB  // diagnostic builds only (NOT bit-exact): no R-digit slab traffic (stale LDS)
+        asm volatile("" ::"v"(pf[0]));
+        return;
+#endif
 #pragma unroll
         for (int m = 0; m < 4; ++m)
             if (tid + 256 * m < SLAB) ash4[buf * SLAB + tid + 256 * m] = pf[m];
     };
     // 4/NG passes of NG 16-sample groups: each A fragment read from LDS feeds 2 NG MFMAs
     constexpr int NG = LGS_OZ_NG;
+#ifdef LGS_DIAG_FAR
+    uint64_t df[8] = {};
+    LGS_DF_T(tf_begin);
+#endif
+#ifdef LGS_OZ_PIPE_PASSES
+    // (round 6, measured and kept out: C3 7.90-8.07 vs 7.86-7.91 ms, C4 11.90-11.94 vs
+    // 11.79-11.81 ms per 2^20, profiles/r06g_kb.log) The passes as one pipelined sequence of (pass, live chunk) items:
+    // the loads of a pass's first chunk (history and R-digit slab) are issued during the
+    // previous pass's last chunk, as within a pass, instead of in a prologue of their
+    // own whose latency nothing hid; each pass's classes are recombined behind the
+    // barrier of its last chunk, while the next item's loads are in flight.
+    {
+        constexpr int NP = 4 / NG;
+        constexpr int NC = kOzDigits + 1;  // digit classes
+        v4i32_t cc[NG][2][NC];  // [group][row tile][class]
+        auto cc_zero = [&]() {
+#pragma unroll
+            for (int q = 0; q < NG; ++q)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) cc[q][t][c] = (v4i32_t){0, 0, 0, 0};
+        };
+        cc_zero();
+        v4i32_t pf[4];
+        v4u_t w[NG][2];
+        auto hist_load = [&](int gp, int ch) {
+            const int16_t* __restrict__ hb0 = a.h16 + (blk0 * a.h16_lanes + p0 + 16 * NG * gp + n) * 16;
+            const v4u_t* h0 = (const v4u_t*)(hb0 + (size_t)ch * hstep);
+            w[0][0] = *(h0);
+            w[0][1] = *(h0 + 1);
+            if constexpr (NG == 2) {
+                const v4u_t* h1 = (const v4u_t*)(hb0 + 16 * 16 + (size_t)ch * hstep);  // group NG gp + 1
+                w[NG - 1][0] = *(h1);
+                w[NG - 1][1] = *(h1 + 1);
+            }
+        };
+        // classes -> fp64; D layout: rows 4h + reg of the tile, sample 16g + n
+        auto epilogue = [&](int gp) {
+#pragma unroll
+            for (int q = 0; q < NG; ++q)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg) {
+                        const int g = NG * gp + q;
+                        const int row = 16 * t + 4 * h + reg;  // panel row = record index
+                        double sv = (double)cc[q][t][NC - 1][reg];
+#pragma unroll
+                        for (int c = NC - 2; c >= 0; --c) sv = fma(sv, 0.00390625, (double)cc[q][t][c][reg]);
+                        const double fv = sv * rec[row * kRecStride + kRecScale];
+                        if (t == 1) {
+#ifdef LGS_XP_ALIAS
+#pragma unroll
+                            for (int gg = 0; gg < 4; ++gg) t1v[gg][reg] = g == gg ? fv : t1v[gg][reg];
+#else
+                            F[(4 * h + reg) * LDF + 16 * g + n] = fv;
+#endif
+                        } else {
+#pragma unroll
+                            for (int gg = 0; gg < 4; ++gg) t0v[gg][reg] = g == gg ? fv : t0v[gg][reg];
+                        }
+                    }
+            cc_zero();
+        };
+        // (no barrier needed first: the panel's record-staging barrier also publishes nzm)
+        const int first = next_live(0);
+        if (first >= nch) {
+#pragma unroll 1
+            for (int gp = 0; gp < NP; ++gp) epilogue(gp);
+        } else {
+            // the item after (g, c): the next live chunk of pass g, else pass g + 1's first
+            auto advance = [&](int& g, int& c) {
+                c = next_live(c + 1);
+                if (c >= nch) {
+                    c = first;
+                    ++g;
+                }
+            };
+            int cgp = 0, cur = first;
+            int ngp = 0, nxt = first;
+            advance(ngp, nxt);
+            slab_load(cur, pf);
+            slab_store(0, pf);
+            if (ngp < NP) slab_load(nxt, pf);
+            hist_load(cgp, cur);
+            __syncthreads();
+#pragma unroll 1
+            for (int it = 0; cgp < NP; ++it) {
+                v4i32_t xh[NG], xl[NG];  // history of chunk cur -> digit planes, per group
+#pragma unroll
+                for (int q = 0; q < NG; ++q) {
+                    const v4u_t w0 = w[q][0], w1 = w[q][1];
+                    xh[q][0] = (int)__builtin_amdgcn_perm(w0[1], w0[0], 0x07050301u);
+                    xh[q][1] = (int)__builtin_amdgcn_perm(w0[3], w0[2], 0x07050301u);
+                    xh[q][2] = (int)__builtin_amdgcn_perm(w1[1], w1[0], 0x07050301u);
+                    xh[q][3] = (int)__builtin_amdgcn_perm(w1[3], w1[2], 0x07050301u);
+                    xl[q][0] = (int)(__builtin_amdgcn_perm(w0[1], w0[0], 0x06040200u) ^ 0x80808080u);
+                    xl[q][1] = (int)(__builtin_amdgcn_perm(w0[3], w0[2], 0x06040200u) ^ 0x80808080u);
+                    xl[q][2] = (int)(__builtin_amdgcn_perm(w1[1], w1[0], 0x06040200u) ^ 0x80808080u);
+                    xl[q][3] = (int)(__builtin_amdgcn_perm(w1[3], w1[2], 0x06040200u) ^ 0x80808080u);
+                }
+                int ngp2 = ngp, nxt2 = nxt;
+                if (ngp < NP) {  // the next item's history; its slab -> LDS, fetch the one after
+                    advance(ngp2, nxt2);
+                    hist_load(ngp, nxt);
+                    slab_store((it + 1) & 1, pf);
+                    if (ngp2 < NP) slab_load(nxt2, pf);
+                }
+                const v4i32_t* sl = ash4 + (it & 1) * SLAB + lane;
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int dg = 0; dg < kOzDigits; ++dg) {
+                        // coarse (wave-uniform): only the kOzCoarse most significant digits
+                        if (dg >= kOzCoarse && coarse) continue;
+                        const v4i32_t av = sl[(t * kOzDigits + dg) * 64];
+                        // digit a = dg + 1: class a - 1 with the high x digit, class a with the low
+#pragma unroll
+                        for (int q = 0; q < NG; ++q) {
+                            cc[q][t][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xh[q], cc[q][t][dg], 0, 0, 0);
+                            cc[q][t][dg + 1] =
+                                __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xl[q], cc[q][t][dg + 1], 0, 0, 0);
+                        }
+                    }
+                __syncthreads();  // next slab complete; this one's reads done before it is reused
+                if (ngp != cgp) epilogue(cgp);  // (the pass's last chunk)
+                cgp = ngp;
+                cur = nxt;
+                ngp = ngp2;
+                nxt = nxt2;
+            }
+        }
+    }
+#else
 #pragma unroll 1
     for (int gp = 0; gp < 4 / NG; ++gp) {
         constexpr int NC = kOzDigits + 1;  // digit classes
@@ -1005,6 +1168,9 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
         // which also publishes nzm)
         int cur = next_live(0);
         int nxt = cur < nch ? next_live(cur + 1) : nch;
+#ifdef LGS_DIAG_FAR
+        LGS_DF_T(tp0);
+#endif
         if (cur < nch) {
             slab_load(cur, pf);
             slab_store(0, pf);
@@ -1012,8 +1178,17 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
             hist_load(cur);
         }
         __syncthreads();
+#ifdef LGS_DIAG_FAR
+        {
+            LGS_DF_T(tp1);
+            df[4] += tp1 - tp0;
+        }
+#endif
 #pragma unroll 1
         for (int it = 0; cur < nch; ++it) {
+#ifdef LGS_DIAG_FAR
+            LGS_DF_T(tc0);
+#endif
             v4i32_t xh[NG], xl[NG];  // history of chunk ch -> digit planes, per group
 #pragma unroll
             for (int q = 0; q < NG; ++q) {
@@ -1027,12 +1202,19 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
                 xl[q][2] = (int)(__builtin_amdgcn_perm(w1[1], w1[0], 0x06040200u) ^ 0x80808080u);
                 xl[q][3] = (int)(__builtin_amdgcn_perm(w1[3], w1[2], 0x06040200u) ^ 0x80808080u);
             }
+#ifdef LGS_DIAG_FAR
+            asm volatile("" ::"v"(xh[NG - 1]), "v"(xl[NG - 1]));
+            LGS_DF_T(tc1);
+#endif
             const int nxt2 = nxt < nch ? next_live(nxt + 1) : nch;
             if (nxt < nch) {  // history of the next live chunk; its slab -> LDS, fetch the one after
                 hist_load(nxt);
                 slab_store((it + 1) & 1, pf);
                 if (nxt2 < nch) slab_load(nxt2, pf);
             }
+#ifdef LGS_DIAG_FAR
+            LGS_DF_T(tc2);
+#endif
             const v4i32_t* sl = ash4 + (it & 1) * SLAB + lane;
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -1042,6 +1224,10 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
                     if (dg >= kOzCoarse && coarse) continue;
                     const v4i32_t av = sl[(t * kOzDigits + dg) * 64];
                     // digit a = dg + 1: class a - 1 with the high x digit, class a with the low
+#ifdef LGS_DIAG_FAR_NOMFMA  // diagnostic builds only (NOT bit-exact): the far field's loads and barriers alone
+                    asm volatile("" ::"v"(av), "v"(xh[NG - 1]), "v"(xl[NG - 1]));
+                    continue;
+#endif
 #pragma unroll
                     for (int q = 0; q < NG; ++q) {
                         cc[q][t][dg] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xh[q], cc[q][t][dg], 0, 0, 0);
@@ -1049,7 +1235,20 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
                             __builtin_amdgcn_mfma_i32_16x16x64_i8(av, xl[q], cc[q][t][dg + 1], 0, 0, 0);
                     }
                 }
+#ifdef LGS_DIAG_FAR
+            LGS_DF_T(tc3);
+#endif
             __syncthreads();  // next slab complete; this one's reads done before it is reused
+#ifdef LGS_DIAG_FAR
+            {
+                LGS_DF_T(tc4);
+                df[0] += tc1 - tc0;
+                df[1] += tc2 - tc1;
+                df[2] += tc3 - tc2;
+                df[3] += tc4 - tc3;
+                df[6] += 1;
+            }
+#endif
             cur = nxt;
             nxt = nxt2;
         }
@@ -1079,6 +1278,7 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
                     }
                 }
     }
+#endif
 #ifdef LGS_XP_ALIAS
     // every pass's chunk loop ended with a block barrier after its last slab reads (and
     // a block without live chunks never touched the slab): F is free for every wave
@@ -1097,6 +1297,16 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
     for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) F[(4 * h + reg) * LDF + 16 * g + n] = t0v[g][reg];
+#ifdef LGS_DIAG_FAR
+    {
+        LGS_DF_T(tf_end);
+        df[7] += 1;
+        // epilogue = the whole call minus prologues and loops
+        df[5] += (tf_end - tf_begin) - df[0] - df[1] - df[2] - df[3] - df[4];
+        if ((threadIdx.x & 63) == 0)
+            for (int k = 0; k < 8; ++k) atomicAdd(&lgs_diag_far[k], (unsigned long long)df[k]);
+    }
+#endif
 }
 
 #ifndef LGS_MFMA_LB32
@@ -1779,7 +1989,11 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     for (int kk = 0; kk < 4; ++kk) {
                         const double av = rx[64 * kk];
                         ZQuad<ZT> q;
+#ifdef LGS_DIAG_COUPLE_NOLOAD  // diagnostic builds only (NOT bit-exact): the coupling without its Z reload
+                        q.load(Z + p0 + 4 * nq);
+#else
                         q.load(zu + (size_t)(4 * kk) * ldz);
+#endif
 #pragma unroll
                         for (int g = 0; g < 4; ++g)
                             c[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, q.get(g), c[g], 0, 0, 0);
@@ -3538,6 +3752,15 @@ extern "C" __attribute__((visibility("default"))) int lgs_diag_cycles_read(unsig
         return -1;
     unsigned long long zero[16] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(lgs::lgs_diag_cycles), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
+#ifdef LGS_DIAG_FAR
+extern "C" __attribute__((visibility("default"))) int lgs_diag_far_read(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lgs::lgs_diag_far), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    unsigned long long zero[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lgs::lgs_diag_far), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif
 #ifdef LGS_DIAG_CAPQ

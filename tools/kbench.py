@@ -42,6 +42,8 @@ def run_one(args):
     dbuf = (ctypes.c_ulonglong * 16)()
     if diag is not None:
         diag(dbuf)  # reset after the warm-up launch
+    if getattr(_capi.load_library(), "lgs_diag_far_read", None) is not None:
+        _capi.load_library().lgs_diag_far_read((ctypes.c_ulonglong * 8)())
     ctx.timing_enable(True)
     for r in range(args.reps):
         ctx.klein(1, (r + 1) * n, n, z, v, lw, flags)
@@ -70,6 +72,15 @@ def run_one(args):
         out["decisions_per_wave"] = {names[3 + k]: round(dbuf[8 + k] / waves, 1) for k in range(5)}
         out["cycles_per_decision"] = {names[3 + k]: round(dbuf[3 + k] / max(dbuf[8 + k], 1), 1)
                                       for k in range(5)}
+    dfar = getattr(_capi.load_library(), "lgs_diag_far_read", None)
+    if dfar is not None:
+        fb = (ctypes.c_ulonglong * 8)()
+        dfar(fb)
+        waves = args.reps * n // 64
+        out["far_cycles_per_wave"] = {nm: round(fb[i] / waves) for i, nm in enumerate(
+            ["hist_wait", "slab_store", "mfma_issue", "barrier", "prologue", "epilogue"])}
+        out["far_chunk_visits_per_wave"] = round(fb[6] / waves, 1)
+        out["far_calls_per_wave"] = round(fb[7] / waves, 1)
     capq = getattr(_capi.load_library(), "lgs_diag_capq_read", None)
     if capq is not None:
         qb = (ctypes.c_ulonglong * 8)()
