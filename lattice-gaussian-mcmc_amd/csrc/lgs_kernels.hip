@@ -976,6 +976,16 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) t1v[g][reg] = 0.0;
 #endif
+    // piece e of the slab is fragment e / 64 = (tile, digit) = ((e / 64) / kOzDigits, (e / 64) % kOzDigits);
+    // a coarse panel's MFMAs read only the kOzCoarse most significant digits: the other
+    // pieces are neither loaded nor staged (LGS_OZ_COARSE_FULL_SLAB: staged, round 5)
+    auto piece_used = [&](int e) {
+#ifndef LGS_OZ_COARSE_FULL_SLAB
+        return e < SLAB && (!coarse || (e >> 6) % kOzDigits < kOzCoarse);
+#else
+        return e < SLAB;
+#endif
+    };
     auto slab_load = [&](int ch, v4i32_t (&pf)[4]) {
 #ifdef LGS_DIAG_FAR_NOSLAB
         ch = 0;
@@ -983,7 +993,7 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
         const v4i32_t* src = rsrc + (size_t)ch * SLAB;
 #pragma unroll
         for (int m = 0; m < 4; ++m)
-            if (tid + 256 * m < SLAB) pf[m] = src[tid + 256 * m];
+            if (piece_used(tid + 256 * m)) pf[m] = src[tid + 256 * m];
     };
     auto slab_store = [&](int buf, const v4i32_t (&pf)[4]) {
 #ifdef LGS_DIAG_FAR_NOSLAB  // diagnostic builds only (NOT bit-exact): no R-digit slab traffic (stale LDS)
@@ -992,7 +1002,7 @@ __device__ __forceinline__ void oz_far_field(const KleinArgs& a, int pk, int p_h
 #endif
 #pragma unroll
         for (int m = 0; m < 4; ++m)
-            if (tid + 256 * m < SLAB) ash4[buf * SLAB + tid + 256 * m] = pf[m];
+            if (piece_used(tid + 256 * m)) ash4[buf * SLAB + tid + 256 * m] = pf[m];
     };
     // 4/NG passes of NG 16-sample groups: each A fragment read from LDS feeds 2 NG MFMAs
     constexpr int NG = LGS_OZ_NG;
@@ -1410,8 +1420,14 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
     // outside speculative sub-panels (+inf once a speculative coordinate is nonzero),
     // and the block's vote for skipping the current panel
     __shared__ double qzs[PB == 32 ? 256 : 1];
+#ifdef LGS_QSKIP_STAGED
     __shared__ int qskip_blk[2];  // (by panel parity: a wave may start the next panel before another
                                   // has read this panel's vote when there is no block barrier between)
+#else
+    // each wave's vote, by panel parity (a wave reaches panel pk + 2 only after every wave
+    // has passed panel pk + 1's barrier, i.e. read panel pk's votes)
+    __shared__ int qvote[2][4];
+#endif
     if constexpr (PB == 32) {
         cert_lds[0][threadIdx.x] = 0.0;
 #ifdef LGS_NEAR_UNROLLED
@@ -1439,6 +1455,8 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
             if constexpr (OZ && !WL)
                 qtry = a.qz2 != nullptr && p_hi >= 32 && ((const __attribute__((address_space(4))) double*)a.qz2)[pk] >= 0.0;
 #endif
+            const int r0 = p_hi - 32;
+#ifdef LGS_QSKIP_STAGED  // (round 5: the panel's records staged before the vote is read)
             // records of coordinates r0 .. r0+31 (r0 = p_hi - 32; negative ones skipped)
             if (qtry && threadIdx.x == 0) qskip_blk[pk & 1] = 1;  // (read last at panel pk - 2: done)
             __syncthreads();
@@ -1447,19 +1465,49 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                 if (__builtin_amdgcn_ballot_w64(active && !(qzs[threadIdx.x] <= q2)) != 0 && lane == 0)
                     qskip_blk[pk & 1] = 0;
             }
-            const int r0 = p_hi - 32;
-            const double2* __restrict__ src = (const double2*)a.crec;
-            double2* dst = (double2*)rec_lds;
-            for (int e = threadIdx.x; e < 32 * kRecStride / 2; e += 256)
-                if (r0 * (kRecStride / 2) + e >= 0) dst[e] = src[(int64_t)r0 * (kRecStride / 2) + e];
-            __syncthreads();
+            bool skip = false;
+            {
+                const double2* __restrict__ src = (const double2*)a.crec;
+                double2* dst = (double2*)rec_lds;
+                for (int e = threadIdx.x; e < 32 * kRecStride / 2; e += 256)
+                    if (r0 * (kRecStride / 2) + e >= 0) dst[e] = src[(int64_t)r0 * (kRecStride / 2) + e];
+                __syncthreads();
+                skip = qtry && __builtin_amdgcn_readfirstlane(qskip_blk[pk & 1]) != 0;
+            }
+#else
+            // (round 6) each wave votes before the barrier that ends the previous panel; a
+            // panel the block skips stages no records (the weight terms are read from the
+            // record array in memory) and needs no second barrier
+            if (qtry) {
+                const double q2 = ((const __attribute__((address_space(4))) double*)a.qz2)[pk];
+                const bool ok = __builtin_amdgcn_ballot_w64(active && !(qzs[threadIdx.x] <= q2)) == 0;
+                if (lane == 0) qvote[pk & 1][wave] = ok ? 1 : 0;
+            }
+            __syncthreads();  // the previous panel's record reads done; the votes visible
+            const bool skip = qtry && __builtin_amdgcn_readfirstlane(qvote[pk & 1][0] & qvote[pk & 1][1] &
+                                                                     qvote[pk & 1][2] & qvote[pk & 1][3]) != 0;
+            if (!skip) {
+                // records of coordinates r0 .. r0+31 (r0 = p_hi - 32; negative ones skipped)
+                const double2* __restrict__ src = (const double2*)a.crec;
+                double2* dst = (double2*)rec_lds;
+                for (int e = threadIdx.x; e < 32 * kRecStride / 2; e += 256)
+                    if (r0 * (kRecStride / 2) + e >= 0) dst[e] = src[(int64_t)r0 * (kRecStride / 2) + e];
+                __syncthreads();
+            }
+#endif
             if (!active) continue;
-            if (qtry && __builtin_amdgcn_readfirstlane(qskip_blk[pk & 1]) != 0) {
+            if (skip) {
                 if (lane == 0) atomicAdd(a.flags + kFlagWordQSkip, 1u);
+                // the 32 weight terms from the contiguous per-coordinate array (one batch of
+                // scalar loads), added in the sequential order
+                const cdptr lt = uniformize(cst(a.lterm) + r0);
+                double ltv[32];
+#pragma unroll
+                for (int s = 0; s < 32; ++s) ltv[s] = lt[31 - s];
 #pragma unroll
                 for (int s = 0; s < 32; ++s) {
                     Z[(size_t)(p_hi - 1 - s) * ldz + p] = (ZT)0;
-                    lw += ((lds_cdptr)rec_lds)[(31 - s) * kRecStride + kRecLterm];  // the sequential order
+                    lw += ltv[s];
                 }
                 v4u_t* hp4 = (v4u_t*)(a.h16 + ((size_t)((p_hi - 32 + a.h16_shift) >> 4) * a.h16_lanes + p) * 16);
                 const v4u_t h128 = (v4u_t){0x00800080u, 0x00800080u, 0x00800080u, 0x00800080u};
