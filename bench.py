@@ -299,10 +299,19 @@ def main():
     if D.collective_active():
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # device memory at the end of the timed region: the whole device's use (library
+    # buffers are hipMalloc'd outside torch's allocator; with LGS_ONE_DEVICE=1 every
+    # rank's buffers are on one device) and torch's own peak, max over ranks
+    free_b, total_b = torch.cuda.mem_get_info(dev)
+    mem_t = [(total_b - free_b) / 2**30, torch.cuda.max_memory_reserved(dev) / 2**30]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed] + mem_t, dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = float(t[0].item())
+        mem_t = [float(t[1].item()), float(t[2].item())]
+    memory = {"device_used_gib": round(mem_t[0], 1), "device_total_gib": round(total_b / 2**30, 1),
+              "torch_peak_reserved_gib_per_rank": round(mem_t[1], 1),
+              "ranks_on_device": world if os.environ.get("LGS_ONE_DEVICE") == "1" else 1}
     step_counter = [shard.next_step]
 
     proposals = args.steps * nc * T * world
@@ -483,6 +492,7 @@ def main():
         "covariance": covariance,
         "roofline": roofline,
         "gemm": gemm,
+        "memory": memory,
         "kernel_ms": {"klein": round(k_ms / max(k_n, 1), 3), "bz": round(g_ms / max(g_n, 1), 3),
                       "accept": round(a_ms / max(a_n, 1), 3), "moments": round(m_ms / max(m_n, 1), 3),
                       "blocks_pipelined": pipelined,
