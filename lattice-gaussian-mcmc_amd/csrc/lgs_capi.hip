@@ -54,6 +54,15 @@ static bool hook_is(const char* name, int v) {
     return e && atoi(e) == v;
 }
 
+// (hooks build) LGS_TEST_NOMEM_ABOVE=bytes: every device allocation above that size fails,
+// as on a full device (tests/test_gpu_edges.py: lgs_imhk's halving of its block)
+#ifdef LGS_TEST_HOOKS
+static size_t test_nomem_above() {  // (read per allocation: tests set and clear it)
+    const char* e = hook("LGS_TEST_NOMEM_ABOVE");
+    return e ? (size_t)atoll(e) : 0;
+}
+#endif
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -68,6 +77,10 @@ struct DevBuf {
             bytes = 0;
         }
         if (need == 0) return LGS_OK;
+#ifdef LGS_TEST_HOOKS
+        if (test_nomem_above() && need > test_nomem_above())
+            return fail(LGS_ERR_NOMEM, "hipMalloc(%zu) refused (LGS_TEST_NOMEM_ABOVE)", need);
+#endif
         hipError_t e = hipMalloc(&p, need);
         if (e != hipSuccess) {
             p = nullptr;

@@ -214,3 +214,52 @@ def test_klein_lattice_points_from_klein_history(capi, oracle):
     assert np.array_equal(r["v"], r["z"].astype(np.float64) @ B.T)
     o = oracle.klein(R, cp, sigma, 16, seed=4321, first_sample=77)
     assert np.array_equal(r["z"][:16], o["z"])
+
+
+def test_imhk_halves_its_block_when_allocation_fails(capi, monkeypatch):
+    """an allocation failure of a block-sized buffer halves lgs_imhk's
+    block (the smaller cap stays with the context) instead of returning LGS_ERR_NOMEM.
+    With every device allocation above 6 MiB refused (hooks build), a 256-chain, 64-step
+    call whose default block (64 steps: a 16 MiB proposal store) does not fit runs in
+    smaller blocks -- pipelined on a caller's stream, and host-checked -- and gives the
+    same chains as an unconstrained context (counter-addressed proposals)."""
+    import torch
+    from conftest import golden_R, load_golden
+    g = load_golden("klein_qary128.npz")
+    R, cp, B = golden_R(g)
+    d, nc, T = R.shape[0], 256, 64
+    dev = "cuda:0"
+
+    def run(ctx, stream):
+        st = dict(z=torch.zeros((d, nc), dtype=torch.int32, device=dev),
+                  lw=torch.zeros(nc, dtype=torch.float64, device=dev),
+                  init=torch.zeros(nc, dtype=torch.int32, device=dev),
+                  acc=torch.zeros(nc, dtype=torch.int64, device=dev),
+                  mom=torch.zeros(2 * d, dtype=torch.int64, device=dev))
+        v = torch.zeros((nc, T, d), dtype=torch.float64, device=dev)
+        s = torch.cuda.Stream(device=dev)
+        torch.cuda.synchronize()
+        if stream:
+            ctx.set_stream(s.cuda_stream)
+        with torch.cuda.stream(s):
+            ctx.imhk(21, 0, nc, 1, T, 1, st["z"], st["lw"], st["init"], st["acc"], v_samples=v, moments=st["mom"],
+                     flags=capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR)
+        torch.cuda.synchronize()
+        return [v.cpu().numpy(), st["z"].cpu().numpy(), st["acc"].cpu().numpy(), st["mom"].cpu().numpy(),
+                st["lw"].cpu().numpy()]
+
+    ref = capi.Context(0, max_proposals=nc * T)
+    ref.set_basis(R, cp, B, float(g["sigma"]))
+    want = run(ref, False)
+    ref.close()
+    for stream in (True, False):
+        ctx = capi.Context(0, max_proposals=nc * T, hooks=True)
+        ctx.set_basis(R, cp, B, float(g["sigma"]))
+        monkeypatch.setenv("LGS_TEST_NOMEM_ABOVE", str(6 << 20))
+        try:
+            got = run(ctx, stream)
+        finally:
+            monkeypatch.delenv("LGS_TEST_NOMEM_ABOVE")
+        ctx.close()
+        for a, b in zip(got, want):
+            assert np.array_equal(a, b)
