@@ -3121,9 +3121,12 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
             *(v4i_t*)&Bs0[row * P + part * 16] = *(const v4i_t*)&Bd0[g];
         }
         __syncthreads();
-        if (mown) {
+        auto moment_partials = [&]() __attribute__((always_inline)) {
             // (round 5) the kept states' moments ride on this tile's digit planes while the
-            // MFMAs run: wave w sums coordinates 16w..16w+15 of the chunk over the tile's 64
+            // MFMAs run (round 6: called after the chunk's MFMAs are issued, so the VALU work
+            // runs under the matrix pipe -- with the 16-byte stores below, B z 7.19 -> 6.98 ms
+            // per 2^22 lattice points, profiles/r06q_bz_ab.log; LGS_BZ_MOM_EARLY: ahead of
+            // them): wave w sums coordinates 16w..16w+15 of the chunk over the tile's 64
             // rows, lane (4 coordinates: lane >> 4) x (4 rows: lane & 15), packed per row as
             // z^2 * 2^24 + (z + 32768) (64 rows: the low field < 2^22, the total < 2^63;
             // rows past n hold z = 0 and add the bias only), then over the 16 lanes of a
@@ -3153,7 +3156,10 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
 #pragma unroll
                 for (int j = 0; j < 4; ++j) mp[j] = ps[j];
             }
-        }
+        };
+#ifdef LGS_BZ_MOM_EARLY
+        if (mown) moment_partials();
+#endif
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int kb = ks * 32 + 16 * (lane >> 5);
@@ -3178,6 +3184,9 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
                 }
             }
         }
+#ifndef LGS_BZ_MOM_EARLY
+        if (mown) moment_partials();
+#endif
         __syncthreads();
     }
     // output rows: sample q -> (q / rb) * rstride + roff + q % rb.  The wave's 32
@@ -3232,6 +3241,41 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
     const int64_t cb = qb / rb;
     const int64_t kb0 = qb - cb * rb;
     const int nrow = (int)min<int64_t>(n - qb, 32);  // valid rows of this tile
+#ifndef LGS_BZ_NARROW
+    // (round 6, with the moments after the MFMAs: B z 7.19 -> 6.98 ms per 2^22 lattice
+    // points, profiles/r06q_bz_ab.log) 16-byte stores: lanes 2c and 2c + 1 swap one value per pair of rows
+    // (DPP quad_perm [1, 0, 3, 2]), so the even lane holds row r, columns 2c and 2c + 1
+    // and the odd lane row r + 1, the same columns
+    if (rb >= 32 && (d & 1) == 0 && (ldv & 1) == 0) {
+        typedef double v2d_t __attribute__((ext_vector_type(2)));
+        const int wrap_row = (int)min<int64_t>(rb - kb0, 32);
+        const bool odd = (lane & 1) != 0;
+        const int c = r0 + wn * (BN / 2) + ((lane & 31) & ~1);
+        double* const vbase = V + (size_t)(cb * rstride + roff + kb0) * ldv + c;
+        const int64_t jump = (rstride - rb) * ldv;
+#pragma unroll
+        for (int reg = 0; reg < 16; reg += 2) {
+            const int row = (reg & 3) + 8 * (reg >> 2) + lrow + (odd ? 1 : 0);
+            double* vrow = vbase + (size_t)row * ldv + (row >= wrap_row ? jump : 0);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const double va = fma((double)p1[ta][tn][reg], 65536.0, (double)p2[ta][tn][reg] * 256.0) +
+                                  (double)p3[ta][tn][reg];
+                const double vb = fma((double)p1[ta][tn][reg + 1], 65536.0, (double)p2[ta][tn][reg + 1] * 256.0) +
+                                  (double)p3[ta][tn][reg + 1];
+                const double send = odd ? va : vb;
+                const unsigned long long sb = __double_as_longlong(send);
+                const unsigned int rlo = (unsigned int)__builtin_amdgcn_mov_dpp((int)(unsigned int)sb, 0xb1, 0xf, 0xf, false);
+                const unsigned int rhi = (unsigned int)__builtin_amdgcn_mov_dpp((int)(unsigned int)(sb >> 32), 0xb1, 0xf, 0xf, false);
+                const double recv = __longlong_as_double((long long)(((unsigned long long)rhi << 32) | rlo));
+                v2d_t o;
+                o[0] = odd ? recv : va;
+                o[1] = odd ? vb : recv;
+                if (row < nrow && c + tn * 32 < d) __builtin_nontemporal_store(o, (v2d_t*)(vrow + tn * 32));
+            }
+        }
+    } else
+#endif
     if (rb >= 32) {
         const int wrap_row = (int)min<int64_t>(rb - kb0, 32);  // first row past the boundary
         double* const vbase = V + (size_t)(cb * rstride + roff + kb0) * ldv + r0 + wn * (BN / 2) + (lane & 31);
