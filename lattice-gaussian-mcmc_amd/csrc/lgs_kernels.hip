@@ -164,6 +164,25 @@ constexpr int kRecHot = 46;  // (with the coarse panels' Cb, read in the batch i
 constexpr int kRecHot = 44;  // through the 15 near-field coefficients and the dispatch code
 #endif
 static_assert(kRecDisp < kRecHot && kRecRs + 15 <= kRecHot && kRecLterm < kRecHot, "hot record fields");
+#ifdef LGS_REC_SMEM
+// (experiment) the record read from the basis' record array in memory through a
+// wave-uniform constant pointer at each use: scalar loads into SGPRs (no LDS reads, no
+// 88 VGPRs holding wave-uniform values)
+struct RecRegs {
+    cdptr p;
+    __device__ __forceinline__ double operator[](int k) const { return p[k]; }
+};
+#elif defined(LGS_REC_RS_SMEM)
+// (experiment) the decision's fields from LDS as before, the 15 near-field coefficients
+// (used last in the step) through scalar loads
+struct RecRegs {
+    double v[kRecHot];
+    cdptr p;
+    __device__ __forceinline__ double operator[](int k) const {
+        return (k >= kRecRs && k < kRecRs + 15) ? p[k] : v[k];
+    }
+};
+#else
 struct RecRegs {
     double v[kRecHot];
 #ifdef LGS_CAP_RI_PRE
@@ -171,20 +190,40 @@ struct RecRegs {
 #endif
     __device__ __forceinline__ double operator[](int k) const { return v[k]; }
 };
+#endif
 struct NoMid {
     __device__ __forceinline__ void operator()() const {}
 };
+#ifdef LGS_REC_SMEM
+__device__ __forceinline__ RecRegs load_rec_g(cdptr grec) { return RecRegs{uniformize(grec)}; }
+#else
 template <typename MID = NoMid>
+#ifdef LGS_REC_RS_SMEM
+__device__ __forceinline__ RecRegs load_rec(lds_cdptr rec, cdptr gp, MID mid = MID{}) {
+#else
 __device__ __forceinline__ RecRegs load_rec(lds_cdptr rec, MID mid = MID{}) {
+#endif
     typedef double d2v __attribute__((ext_vector_type(2)));
     using lds_d2p = const __attribute__((address_space(3))) d2v*;
     RecRegs r;
+#ifdef LGS_REC_RS_SMEM
+    static_assert(kRecRs % 2 == 0 && kRecDisp == kRecRs + 15 && kRecHot == kRecDisp + 1, "record layout");
+#pragma unroll
+    for (int k = 0; k < kRecHot / 2; ++k) {
+        if (2 * k >= kRecRs && 2 * k + 1 < kRecRs + 15) continue;
+        const d2v t = ((lds_d2p)rec)[k];
+        r.v[2 * k] = t[0];
+        r.v[2 * k + 1] = t[1];
+    }
+    r.p = uniformize(gp);
+#else
 #pragma unroll
     for (int k = 0; k < kRecHot / 2; ++k) {
         const d2v t = ((lds_d2p)rec)[k];
         r.v[2 * k] = t[0];
         r.v[2 * k + 1] = t[1];
     }
+#endif
     mid();
 #ifdef LGS_CAP_RI_PRE
     r.ri = load_cap_ri();
@@ -210,11 +249,14 @@ __device__ __forceinline__ RecRegs load_rec(lds_cdptr rec, MID mid = MID{}) {
     for (int k = 0; k < kRecHot; ++k)
 #ifdef LGS_REC_L2  // (Rs[1..14] not pinned: the first use waits for them)
         if (k <= kRecRs)
+#elif defined(LGS_REC_RS_SMEM)
+        if (k < kRecRs || k >= kRecRs + 14)
 #endif
             asm volatile("" : "+v"(r.v[k]));
 #endif
     return r;
 }
+#endif
 #ifdef LGS_REC_L2
 #define REC_CBC rr[kRecCbC]
 #else
@@ -222,7 +264,7 @@ __device__ __forceinline__ RecRegs load_rec(lds_cdptr rec, MID mid = MID{}) {
 #endif
 struct RecView {  // q[k] of the SampleZ functions, served from the registers
     const RecRegs& r;
-    __device__ __forceinline__ double operator[](int k) const { return r.v[k]; }
+    __device__ __forceinline__ double operator[](int k) const { return r[k]; }
 };
 
 // decide_coord with the coordinate's record rec staged in LDS (klein_mfma_kernel,
@@ -1824,6 +1866,10 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     // the same placement as an optimisation) the coordinate's Philox block drawn
                     // under the record's LDS reads, off the decision's dependency chain
                     const RecRegs rr = load_rec(rec, [&]() { (void)rs.u((uint32_t)(d - 1 - i)); });
+#elif defined(LGS_REC_SMEM)
+                    const RecRegs rr = load_rec_g(cst(a.crec) + (size_t)i * kRecStride);
+#elif defined(LGS_REC_RS_SMEM)
+                    const RecRegs rr = load_rec(rec, cst(a.crec) + (size_t)i * kRecStride);
 #else
                     const RecRegs rr = load_rec(rec);
 #endif
