@@ -3291,8 +3291,9 @@ __global__ __launch_bounds__(256, LGS_BZ_OCC) void bz_i8_kernel(const ZT* __rest
     // (round 6, with the moments after the MFMAs: B z 7.19 -> 6.98 ms per 2^22 lattice
     // points, profiles/r06q_bz_ab.log) 16-byte stores: lanes 2c and 2c + 1 swap one value per pair of rows
     // (DPP quad_perm [1, 0, 3, 2]), so the even lane holds row r, columns 2c and 2c + 1
-    // and the odd lane row r + 1, the same columns
-    if (rb >= 32 && (d & 1) == 0 && (ldv & 1) == 0) {
+    // and the odd lane row r + 1, the same columns (even d and ldv, V 16-byte aligned: every
+    // pair then starts on a 16-byte boundary; otherwise the 8-byte stores below)
+    if (rb >= 32 && (d & 1) == 0 && (ldv & 1) == 0 && ((uintptr_t)V & 15) == 0) {
         typedef double v2d_t __attribute__((ext_vector_type(2)));
         const int wrap_row = (int)min<int64_t>(rb - kb0, 32);
         const bool odd = (lane & 1) != 0;

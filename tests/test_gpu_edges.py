@@ -200,6 +200,36 @@ def test_imhk_lattice_points_from_klein_history(capi, oracle, wl):
         assert 0 < a.sum() < 2 * T * nc  # some chains kept a carried-in state
 
 
+def test_lattice_points_into_8_byte_aligned_output(capi, oracle):
+    """B z writes 16 bytes per lane (two coordinates of a row) when d, the row pitch and
+    the output pointer allow it, 8 bytes otherwise: an output that starts one double into
+    its allocation (8-byte aligned only) gets the same lattice points as an aligned one."""
+    import torch
+    from lgs_amd.lattices import build_config
+    lat, sigma = build_config("C2_qary128")
+    B = lat.basis
+    R, cp = oracle.qr_prepare(B)
+    ctx = capi.Context(0)
+    ctx.set_basis(R, cp, B, sigma)
+    d, n = B.shape[0], 1024
+    f = capi.LGS_DEVICE_PTRS | capi.LGS_COORD_MAJOR
+    out = []
+    for off in (0, 1):
+        z = torch.zeros((d, n), dtype=torch.int32, device="cuda:0")
+        lw = torch.zeros(n, dtype=torch.float64, device="cuda:0")
+        buf = torch.full((n * d + 2,), -1.0, dtype=torch.float64, device="cuda:0")
+        v = buf[off:off + n * d].view(n, d)
+        assert (v.data_ptr() % 16 == 0) == (off == 0)
+        ctx.klein(5, 0, n, z, v, lw, f)
+        torch.cuda.synchronize()
+        zn = z.cpu().numpy().T.astype(np.float64)
+        assert np.array_equal(v.cpu().numpy(), zn @ B.T)
+        b = buf.cpu().numpy()
+        assert np.all(b[:off] == -1.0) and np.all(b[off + n * d:] == -1.0)  # nothing outside
+        out.append(v.cpu().numpy())
+    assert np.array_equal(out[0], out[1])
+
+
 def test_klein_lattice_points_from_klein_history(capi, oracle):
     """lgs_klein with lattice points (NTRU d = 1024, 512 samples: int8-digit far
     field): B z from the launch's history equals B z of the returned coefficients,
