@@ -6,6 +6,7 @@ cd "$(dirname "$0")/../lattice-gaussian-mcmc_amd"
 name=$1; shift
 mkdir -p build/var
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-pass-failed \
-  -mllvm -pragma-unroll-threshold=200000 -DLGS_TEST_HOOKS "$@" -shared -o build/var/$name.so \
+  -mllvm -pragma-unroll-threshold=200000 -mllvm -amdgpu-use-amdgpu-trackers=1 -mllvm -amdgpu-schedule-metric-bias=50 \
+  -DLGS_TEST_HOOKS "$@" -shared -o build/var/$name.so \
   csrc/lgs_kernels.hip csrc/lgs_diag.hip csrc/lgs_capi.hip
 echo built build/var/$name.so
