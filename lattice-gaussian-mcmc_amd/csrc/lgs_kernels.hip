@@ -1833,8 +1833,14 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
 #pragma unroll
                 for (int j = 0; j < 8; ++j) hp[j] = 0u;
                 int flm = 0;
-#ifdef LGS_CAP_SP
-                // the whole sub-panel is capped with sigma >= 360 (host flag kRecSpec == 2)
+#ifndef LGS_NO_CAP_SP
+                // the whole sub-panel is capped with sigma >= 360 (host flag kRecSpec == 2):
+                // its steps take the capped decision without the per-coordinate kind
+                // dispatch (round 6, with the scheduler flags: C3 / C4 / C5 Klein -2.9 / -1.2
+                // / -1.6 %, the bench 114.1 -> 116.8 M samples/s, identical hashes,
+                // profiles/r06al_capsp.log; round 5, without them: neutral).  Such a
+                // sub-panel is never in a coarse panel (two kRecSpec == 1 sub-panels), so
+                // its certificate uses the sub-panel's own Cb.
                 const int capsp = !LIBM && rows16 == 16 &&
                                   __builtin_amdgcn_readfirstlane((int)((lds_cdptr)rec_lds)[(top - 1 - (p_hi - 32)) * kRecStride + kRecSpec]) == 2;
 #endif
@@ -1876,7 +1882,7 @@ __global__ __launch_bounds__(256, PB == 32 ? (OZ ? LGS_OZ_LB : LGS_MFMA_LB32) : 
                     const double mu = (rr[kRecCp] - acc[15]) * rr[kRecIrii];
                     LGS_DC_T(t_sz0);
                     bool un;
-#ifdef LGS_CAP_SP
+#ifndef LGS_NO_CAP_SP
                     int cf = __builtin_amdgcn_readfirstlane(capsp);
                     asm volatile("" : "+s"(cf));  // a scalar test per step (no loop unswitching: one copy of the loop)
                     const double zi = cf ? decide_capped_rec<WL>(a, i, mu, rec, rr, rs, lw, flags, etab_s,
