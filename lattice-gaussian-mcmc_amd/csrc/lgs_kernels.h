@@ -4,6 +4,27 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Round-6 defaults of the Klein kernel's near field, measured together under the
+// scheduler flags (Makefile) with identical outputs: the record laid out decision-first
+// with its near-field coefficients read last (LGS_REC_L2), the record's LDS reads left
+// to the scheduler instead of pinned per register (LGS_REC_NOPIN), and the Philox round
+// keys left to loop-invariant motion (LGS_PHILOX_HOIST).  Each alone is within noise;
+// together the bench 117.0-117.4 -> 118.9-119.6 M samples/s and Klein 28.84-28.93 ->
+// 28.20-28.34 ms per 2^22 block (profiles/r06au_bench_variants.log), C3 / C4 / C5 Klein
+// -1.6 / -1.0 / -1.3 % at 2^20 samples and C1 / C2 +1.7 / +1.2 % (r06av_call_kbench.log).
+// LGS_R6_OFF restores the round-5 forms.
+#ifndef LGS_R6_OFF
+#ifndef LGS_REC_L2
+#define LGS_REC_L2 1
+#endif
+#ifndef LGS_REC_NOPIN
+#define LGS_REC_NOPIN 1
+#endif
+#ifndef LGS_PHILOX_HOIST
+#define LGS_PHILOX_HOIST 1
+#endif
+#endif
+
 namespace lgs {
 
 constexpr unsigned int kFlagNonFinite = 1u;  // a conditional mean was NaN/inf
