@@ -260,7 +260,8 @@ def main():
     # LGS_NO_PIPE=1 (read here, passed as lgs_create_ex's LGS_CTX_NO_PIPELINE): isolated
     # launches, for the rocprof roofline passes (tools/gpu_roofline.sh)
     pipelined = os.environ.get("LGS_NO_PIPE") != "1"
-    ctx = _capi.Context(local, pipeline=pipelined)
+    # LGS_NO_CU_SPLIT=1 (lgs_create_ex's LGS_CTX_NO_CU_SPLIT): the Klein stream on every CU, A/B
+    ctx = _capi.Context(local, pipeline=pipelined, cu_split=os.environ.get("LGS_NO_CU_SPLIT") != "1")
     ctx.set_basis(R, cp, B, sigma)
     nc = args.chains or WORKLOADS[args.config]["chains"]
     T = args.imhk_steps
@@ -496,10 +497,12 @@ def main():
         "kernel_ms": {"klein": round(k_ms / max(k_n, 1), 3), "bz": round(g_ms / max(g_n, 1), 3),
                       "accept": round(a_ms / max(a_n, 1), 3), "moments": round(m_ms / max(m_n, 1), 3),
                       "blocks_pipelined": pipelined,
+                      "klein_stream_cus": ctx.counter(_capi.LGS_COUNTER_KLEIN_CUS) or dinfo.get("n_cu"),
                       "note": "pipelined blocks: each lgs_imhk block's Klein launch runs on the library's Klein "
                               "stream beside the previous block's accept / moments / B z on the work stream, so "
                               "these launch times overlap (their sum exceeds ms_per_step) and each is stretched by "
-                              "sharing the CUs; LGS_NO_PIPE=1 gives isolated launches"},
+                              "sharing the CUs; the Klein stream's queue is masked to klein_stream_cus CUs "
+                              "(1/8 of them left to B z); LGS_NO_PIPE=1 gives isolated launches"},
         "cpu_baseline": cpu,
         "wang_ling": wang_ling,
         "device": dinfo["name"],

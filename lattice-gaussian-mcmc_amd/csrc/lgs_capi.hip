@@ -183,7 +183,7 @@ struct lgs_ctx {
         stage_f, stage_g, stage_h, stage_i, vs;
     int64_t max_props = 1 << 18;
     bool max_props_user = false;  // lgs_create_ex's cap (else set per basis, lgs_set_basis)
-    bool no_pipe = false, no_look = false, no_qskip = false;  // lgs_create_ex ctx_flags
+    bool no_pipe = false, no_look = false, no_qskip = false, no_cu_split = false;  // lgs_create_ex ctx_flags
     int zint = 2;  // internal coefficient store width (bytes): 16-bit, sticky 32-bit on overflow; LGS_ZINT=4 forces 32-bit
     // timing
     bool timing = false;
@@ -215,6 +215,16 @@ struct lgs_ctx {
     int nsets = 2;  // buffer sets in rotation (LGS_PIPE_SETS=3: three, fixed at the first pipelined call)
     bool kstream_sets_fixed = false;
     hipStream_t kstream = nullptr;
+    // CU split (lgs_imhk, pipelined): kstream is kstream_full (every CU) or kstream_split
+    // (its queue masked off 1/8 of the CUs).  cu_split: 0 undecided (the first pipelined
+    // Klein launch is timed on kstream_full, kt0 / kt1), 1 split, 2 every CU.
+    hipStream_t kstream_full = nullptr, kstream_split = nullptr;
+    int cu_split = 0;
+    int kstream_cus = 0;  // CUs in kstream's mask (0: all)
+    int split_cus = 0;    // CUs in kstream_split's mask
+    hipEvent_t kt0 = nullptr, kt1 = nullptr;
+    bool kt_pending = false;
+    double kt_bz_ms = 0.0;  // the timed block's B z store estimate
     hipEvent_t ev_klein = nullptr;
     // Look-ahead: at the end of a pipelined call, the Klein launch of the next call's
     // first block as this call predicts it (same seed, chains, steps per call, store;
@@ -325,6 +335,32 @@ struct SetSwap {
     }
     ~SetSwap() { release(); }
 };
+
+// The CU split's decision (lgs_ctx::cu_split), once, after the first pipelined call
+// whose timed Klein launch (every CU, kt0 -> kt1) has finished: the split costs the
+// Klein launches cu_res / split_cus of their time (1/7) and hides the previous block's
+// B z behind them, so it is taken when that block's B z -- its lattice-point stores,
+// 8 d bytes per kept proposal at the ~4.6 TB/s bz_i8_kernel reaches on MI355X -- is the
+// larger.  Measured (bench, same box, profiles/r06bc_bench_cusplit_ab.log): C3 0.26 of
+// the Klein time, split +3.0 %; C4 0.16, +1.6 %; C5 0.13, -3.4 %; C2 0.09, -3.6 %.
+constexpr double kBzStoreBytesPerMs = 4.6e9;
+static int split_decide(lgs_ctx* c) {
+    if (c->cu_split != 0 || !c->kt_pending || hipEventQuery(c->kt1) != hipSuccess) return LGS_OK;
+    c->kt_pending = false;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->kt0, c->kt1) != hipSuccess || !(ms > 0.f)) return LGS_OK;  // (timed again)
+    const int ncu = c->split_cus * 8 / 7;
+    const double cost = (double)ms * (double)(ncu - c->split_cus) / (double)c->split_cus;
+    if (c->kt_bz_ms > cost) {
+        HIP_TRY(hipStreamSynchronize(c->kstream_full));  // (idle but for an early look-ahead launch)
+        c->kstream = c->kstream_split;
+        c->kstream_cus = c->split_cus;
+        c->cu_split = 1;
+    } else {
+        c->cu_split = 2;
+    }
+    return LGS_OK;
+}
 
 // Drops a look-ahead Klein launch (lgs_ctx::Spec): waits for it and clears the flag
 // words it wrote into its set.
@@ -811,6 +847,7 @@ int lgs_create_ex(lgs_ctx** out, int device, int64_t max_proposals, uint32_t ctx
     c->no_pipe = (ctx_flags & LGS_CTX_NO_PIPELINE) != 0;
     c->no_look = (ctx_flags & LGS_CTX_NO_LOOKAHEAD) != 0;
     c->no_qskip = (ctx_flags & LGS_CTX_NO_QSKIP) != 0;
+    c->no_cu_split = (ctx_flags & LGS_CTX_NO_CU_SPLIT) != 0;
     if (max_proposals > 0) {
         c->max_props = std::max<int64_t>(64, max_proposals);
         c->max_props_user = true;
@@ -892,10 +929,13 @@ int lgs_destroy(lgs_ctx* c) {
     for (auto e : c->pool) (void)hipEventDestroy(e);
     if (c->fw_ev) (void)hipEventDestroy(c->fw_ev);
     if (c->fw_host) (void)hipHostFree(c->fw_host);
-    if (c->kstream) {
-        (void)hipStreamSynchronize(c->kstream);
-        (void)hipStreamDestroy(c->kstream);
-    }
+    for (hipStream_t ks : {c->kstream_full, c->kstream_split})
+        if (ks) {
+            (void)hipStreamSynchronize(ks);
+            (void)hipStreamDestroy(ks);
+        }
+    if (c->kt0) (void)hipEventDestroy(c->kt0);
+    if (c->kt1) (void)hipEventDestroy(c->kt1);
     if (c->ev_klein) (void)hipEventDestroy(c->ev_klein);
     if (c->spec.ev) (void)hipEventDestroy(c->spec.ev);
     for (auto& s : c->bset)
@@ -932,6 +972,13 @@ int lgs_set_basis(lgs_ctx* c, int64_t d, const double* R, const double* cprime, 
     // copies below are not ordered after a non-blocking stream's work
     HIP_TRY(hipStreamSynchronize(c->stream));
     if ((rc = spec_discard(c))) return rc;  // (a look-ahead launch reads the basis being replaced)
+    if (c->kstream_split && c->cu_split != 0 && !hook("LGS_PIPE_CU_RESERVE")) {  // the CU split decided anew
+        HIP_TRY(hipStreamSynchronize(c->kstream));
+        c->kstream = c->kstream_full;
+        c->kstream_cus = 0;
+        c->cu_split = 0;
+    }
+    c->kt_pending = false;
     const int PB = c->panel;
     const size_t dd = (size_t)d;
     // per-coordinate parameters (klein.py:195-211, 255-263)
@@ -1529,11 +1576,51 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             // 102.6-102.9 M samples/s at the default priority, profiles/r05k_*);
             // 2: at the lowest, so the previous block's dependants go first
             static const int prio = hook("LGS_PIPE_PRIO") ? atoi(hook("LGS_PIPE_PRIO")) : 0;
-            int plo = 0, phi = 0;
+            // CU split (default; LGS_CTX_NO_CU_SPLIT turns it off): a second Klein stream
+            // whose queue is masked off 1/8 of the CUs, so the previous block's
+            // store-bound B z finds CUs beside the Klein launch, which otherwise fills
+            // every CU's VGPRs and LDS (B z then runs behind it, ~3 % overlap).  Mask bit
+            // i is a CU of XCD i % 8 and shader engine (i / 8) % 4, so the top ncu / 8
+            // bits take one CU from every shader engine -- an even cut, which the per-SE
+            // round-robin workgroup dispatch needs (uneven masks run at the pace of the
+            // smallest SE: 16 or 48 spread bits 2x / 1.3x slower,
+            // profiles/r06ba_bench_cumask.log; 1/16, 3/32 or 5/32 of the CUs at the top
+            // less or slower, r06bb_*).  Which stream is used is decided after the
+            // first pipelined call (split_decide).
+            // (hooks build: LGS_PIPE_CU_RESERVE=k forces the split with the top k bits,
+            // 0 = never; LGS_PIPE_CU_PAT=0 k bits spread over the index space instead)
+            const char* h_res = hook("LGS_PIPE_CU_RESERVE");
+            static const int cu_pat = hook("LGS_PIPE_CU_PAT") ? atoi(hook("LGS_PIPE_CU_PAT")) : 1;
+            int plo = 0, phi = 0, ncu = 0;
+            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) ncu = 0;
+            const int cu_res = h_res ? atoi(h_res) : (c->no_cu_split || ncu % 32 != 0 ? 0 : ncu / 8);
             if (prio && hipDeviceGetStreamPriorityRange(&plo, &phi) == hipSuccess && phi != plo)
-                HIP_TRY(hipStreamCreateWithPriority(&c->kstream, hipStreamNonBlocking, prio == 1 ? phi : plo));
+                HIP_TRY(hipStreamCreateWithPriority(&c->kstream_full, hipStreamNonBlocking, prio == 1 ? phi : plo));
             else
-                HIP_TRY(hipStreamCreateWithFlags(&c->kstream, hipStreamNonBlocking));
+                HIP_TRY(hipStreamCreateWithFlags(&c->kstream_full, hipStreamNonBlocking));
+            c->kstream = c->kstream_full;
+            c->kstream_cus = 0;
+            c->cu_split = 2;
+            if (cu_res > 0 && cu_res < ncu) {
+                std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+                const int stride = std::max(1, ncu / cu_res);
+                int off = 0;
+                for (int i = 0; i < ncu; ++i) {
+                    const bool res = cu_pat == 1 ? i >= ncu - cu_res : (i % stride == stride - 1 && off < cu_res);
+                    if (res && cu_pat != 1) ++off;
+                    if (!res) mask[i / 32] |= 1u << (i % 32);
+                }
+                HIP_TRY(hipExtStreamCreateWithCUMask(&c->kstream_split, (uint32_t)mask.size(), mask.data()));
+                HIP_TRY(hipEventCreate(&c->kt0));
+                HIP_TRY(hipEventCreate(&c->kt1));
+                c->split_cus = ncu - cu_res;
+                c->cu_split = 0;
+                if (h_res) {  // (forced)
+                    c->cu_split = 1;
+                    c->kstream = c->kstream_split;
+                    c->kstream_cus = c->split_cus;
+                }
+            }
             HIP_TRY(hipEventCreateWithFlags(&c->ev_klein, hipEventDisableTiming));
         }
         if (!c->kstream_sets_fixed) {
@@ -1731,10 +1818,17 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
             auto& bs = c->bset[sw.j];
             if (bs.free_recorded) HIP_TRY(hipStreamWaitEvent(c->kstream, bs.ev_free, 0));
             const hipStream_t cs = c->stream;
+            const bool timed = c->cu_split == 0 && !c->kt_pending;  // (the CU split's measurement)
+            if (timed) HIP_TRY(hipEventRecord(c->kt0, c->kstream));
             c->stream = c->kstream;
             rc = run_klein_store(c, a, exact, wl, zb, c->Z.p, true, &ozb);
             c->stream = cs;
             if (rc) return rc;
+            if (timed) {
+                HIP_TRY(hipEventRecord(c->kt1, c->kstream));
+                c->kt_pending = true;
+                c->kt_bz_ms = carry ? (double)nc * (double)kb * 8.0 * (double)d / kBzStoreBytesPerMs : 0.0;
+            }
             HIP_TRY(hipEventRecord(c->ev_klein, c->kstream));
             HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_klein, 0));
         } else if ((rc = run_klein_store(c, a, exact, wl, zb, c->Z.p, true, &ozb))) {
@@ -1909,6 +2003,7 @@ static int imhk_impl(lgs_ctx* c, uint64_t seed, uint64_t first_chain, int64_t nc
         if (redo) continue;  // same block again (block 0: its initial draws too)
         t0 += T;
     }
+    if (pipe && (rc = split_decide(c))) return rc;
     if (pipe && !no_look && look_late && next_step + (uint64_t)n_steps <= (1ull << 32))
         if ((rc = lookahead(c, c->bset_next, seed, first_chain, next_step, nc, std::min<int64_t>(T, n_steps), carry, zb,
                             exact, wl)))
@@ -1994,8 +2089,12 @@ int lgs_timing_get(lgs_ctx* c, int kernel, double* ms, int64_t* n) {
 
 int lgs_counter(lgs_ctx* c, int which, int reset, uint64_t* value) {
     if (!c) return fail(LGS_ERR_INVALID, "null context");
-    if (which < LGS_COUNTER_RESOLVED || which > LGS_COUNTER_QSKIP)
-        return fail(LGS_ERR_INVALID, "counter id 0..4");
+    if (which < LGS_COUNTER_RESOLVED || which > LGS_COUNTER_KLEIN_CUS)
+        return fail(LGS_ERR_INVALID, "counter id 0..5");
+    if (which == LGS_COUNTER_KLEIN_CUS) {
+        if (value) *value = (uint64_t)c->kstream_cus;
+        return LGS_OK;
+    }
     uint64_t& v = which == LGS_COUNTER_RESOLVED      ? c->n_resolved
                   : which == LGS_COUNTER_FALLBACK    ? c->n_fallback
                   : which == LGS_COUNTER_ACCEPT_RESOLVED ? c->n_accept_resolved

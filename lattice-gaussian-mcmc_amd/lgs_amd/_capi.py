@@ -47,6 +47,7 @@ LGS_CTX_PANEL16 = 0x8
 LGS_CTX_FAR_FP64 = 0x10
 LGS_CTX_STORE32 = 0x20
 LGS_CTX_NO_QSKIP = 0x40
+LGS_CTX_NO_CU_SPLIT = 0x80
 
 KERNEL_KLEIN, KERNEL_BZ, KERNEL_ACCEPT, KERNEL_MOMENTS = 0, 1, 2, 3
 KERNEL_GRAM, KERNEL_SERIES, KERNEL_KLEIN_INIT = 4, 5, 6
@@ -55,6 +56,7 @@ LGS_COUNTER_FALLBACK = 1
 LGS_COUNTER_ACCEPT_RESOLVED = 2
 LGS_COUNTER_WL_MISMATCH = 3
 LGS_COUNTER_QSKIP = 4
+LGS_COUNTER_KLEIN_CUS = 5
 
 # every symbol include/lgs.h declares (checked by tests/test_capi_symbols.py)
 EXPORTS = ("lgs_version", "lgs_last_error", "lgs_create", "lgs_create_ex", "lgs_destroy", "lgs_set_stream",
@@ -217,7 +219,8 @@ class Context:
 
     def __init__(self, device: int = 0, *, max_proposals: int = 0, pipeline: bool = True,
                  lookahead: bool = True, samplez_libm: bool = False, panel: int = 32, far: str = "int8",
-                 store32: bool = False, qskip: bool = True, hooks: bool = False):
+                 store32: bool = False, qskip: bool = True, cu_split: bool = True,
+                 hooks: bool = False):
         """lgs_create_ex: max_proposals (0 = the library's default) and the LGS_CTX_*
         options; hooks=True loads liblgs_hip_hooks.so (the environment's test switches)."""
         L = load_library(HOOKS_LIB_PATH if hooks else LIB_PATH)
@@ -225,7 +228,7 @@ class Context:
         flags = ((0 if pipeline else LGS_CTX_NO_PIPELINE) | (0 if lookahead else LGS_CTX_NO_LOOKAHEAD) |
                  (LGS_CTX_SAMPLEZ_LIBM if samplez_libm else 0) | (LGS_CTX_PANEL16 if panel == 16 else 0) |
                  (LGS_CTX_FAR_FP64 if far == "fp64" else 0) | (LGS_CTX_STORE32 if store32 else 0) |
-                 (0 if qskip else LGS_CTX_NO_QSKIP))
+                 (0 if qskip else LGS_CTX_NO_QSKIP) | (0 if cu_split else LGS_CTX_NO_CU_SPLIT))
         if panel not in (16, 32) or far not in ("int8", "fp64"):
             raise ValueError("panel is 16 or 32, far is 'int8' or 'fp64'")
         h = _vp()

@@ -373,7 +373,7 @@ def test_early_check_equals_synchronised_call(capi, zmax):
 
 
 def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, blocks: int = 3, plan=None,
-                thin: int = 1, z64: bool = False):
+                thin: int = 1, z64: bool = False, cu_split: bool = True, gauge=None, hooks: bool = False):
     """Several lgs_imhk_ex calls of several blocks each (max_proposals: T = 4 steps
     per block), chain state, accept counts, moments, lattice points, functionals and
     lag sums carried across them -- on a caller's stream the blocks are pipelined
@@ -384,7 +384,7 @@ def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, 
     g = load_golden("klein_qary128.npz")
     R, cp, B = golden_R(g)
     d, nc, T = R.shape[0], 256, 4
-    ctx = capi.Context(0, max_proposals=nc * T)
+    ctx = capi.Context(0, max_proposals=nc * T, cu_split=cu_split, hooks=hooks)
     ctx.set_basis(R, cp, B, float(g["sigma"]))
     dev = "cuda:0"
     plan = plan or [T * blocks] * calls  # steps per call (a changed count discards the look-ahead launch)
@@ -426,6 +426,8 @@ def _imhk_calls(capi, on_caller_stream: bool, flags_extra: int, calls: int = 3, 
     out["v"] = torch.cat(vs_all, 1).cpu().numpy()
     out["vn2"] = torch.cat(vn_all, 1).cpu().numpy()
     out["zk"] = torch.cat(zk_all, 1).cpu().numpy()
+    if gauge is not None:
+        gauge.append((ctx.counter(capi.LGS_COUNTER_KLEIN_CUS), ctx.device_info()["n_cu"]))
     ctx.close()
     return B, out
 
@@ -454,6 +456,29 @@ def test_pipelined_blocks_equal_synchronised_calls(capi, mode, plan, thin, z64):
     # moments: sum over every kept state of z and z^2 (exact integers)
     assert np.array_equal(a["mom"][:B.shape[0]], zrec.astype(np.int64).sum(0))
     assert np.array_equal(a["mom"][B.shape[0]:], (zrec.astype(np.int64) ** 2).sum(0))
+
+
+def test_cu_split_klein_stream_equals_unmasked(capi, monkeypatch):
+    """The pipelined Klein launches on a stream whose queue is masked off 1/8 of the CUs
+    (forced here through the hooks build's LGS_PIPE_CU_RESERVE; by default the library
+    takes it when the B z stores outweigh 1/7 of the timed Klein launch) give every
+    output of the launches on every CU (LGS_CTX_NO_CU_SPLIT); LGS_COUNTER_KLEIN_CUS
+    reports the mask.  Without the hook, this small lattice (d = 128: B z is a tenth of
+    the Klein time) keeps every CU."""
+    import torch
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    res = ncu // 8 if ncu % 32 == 0 else 0
+    g1, g2, g3 = [], [], []
+    monkeypatch.setenv("LGS_PIPE_CU_RESERVE", str(res))
+    _, a = _imhk_calls(capi, True, 0, gauge=g1, hooks=True)
+    monkeypatch.delenv("LGS_PIPE_CU_RESERVE")
+    _, b = _imhk_calls(capi, True, 0, cu_split=False, gauge=g2)
+    _, c = _imhk_calls(capi, True, 0, gauge=g3)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+        assert np.array_equal(a[k], c[k]), k
+    assert g1[0] == ((ncu - res) if res else 0, ncu)
+    assert g2[0][0] == 0 and g3[0][0] in (0, ncu - res)
 
 
 def test_lookahead_discarded_on_new_basis_and_changed_call(capi):
